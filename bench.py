@@ -1,0 +1,223 @@
+#!/usr/bin/env python3
+"""Headline benchmark: decoded codewords/s (+ info-bits/s) of the on-device
+Monte-Carlo step on MI355X, BASELINE.json configs[1]:
+
+    WiMAX n=576 rate-1/2 (wimax_576_0.5), SPA fp64, max 50 iterations with the
+    reference's early-termination syndrome, 65,536 frames per GPU per step,
+    reference SNR axis 0 dB (speed 1.0).
+
+A step = one pass of the hot path over one batch: generate 65,536 synthetic
+frames on the GPU (info bits -> [u, A.u] -> BPSK -> AWGN -> LLR), decode them
+(CN + VN/syndrome kernels, up to 50 iterations) and reduce the five
+main.py counters on the device.  With N GPUs (one process per GPU, launched by
+torch.distributed.run) every rank decodes its own disjoint frame range and the
+counters are summed with ONE all-reduce over RCCL (weak scaling).
+
+Output: ONE JSON line on rank 0 (contract in the task statement), with
+`roofline` for the dominant kernel (cn_kernel, timed live with HIP events on
+its own stream) and `cpu_baseline` (the C oracle, OpenMP, bounded sample).
+"""
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "ldpc-simulator_amd"))
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+SEED = 20260213
+METRIC = "decoded codewords/s + info-bits/s at fixed (N, rate, max_iter, Eb/N0)"
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--code", default="wimax_576_0.5")
+    ap.add_argument("--frames", type=int, default=65536, help="frames per GPU per step")
+    ap.add_argument("--chunk", type=int, default=0, help="decoder chunk (frames); 0 = whole batch")
+    ap.add_argument("--iters", type=int, default=50)
+    ap.add_argument("--snr", type=float, default=0.0, help="reference SNR axis (dB), speed=1")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU-baseline sample budget (0 = skip)")
+    ap.add_argument("--cpu-threads", type=int, default=0)
+    return ap.parse_args()
+
+
+def dist_setup(args):
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl")  # RCCL on ROCm
+    return world, rank, local, dist
+
+
+def allreduce_counters(dist, ctr, local):
+    """The single RCCL all-reduce of the error counters (int64 vector)."""
+    if dist is None:
+        return ctr
+    import torch
+    t = torch.from_numpy(ctr.reshape(-1).copy()).to(f"cuda:{local}")
+    dist.all_reduce(t)
+    return t.cpu().numpy().reshape(ctr.shape)
+
+
+def barrier(dist, local):
+    if dist is not None:
+        import torch
+        dist.barrier()
+        torch.cuda.synchronize(local)
+
+
+def max_over_ranks(dist, x, local):
+    if dist is None:
+        return x
+    import torch
+    t = torch.tensor([x], dtype=torch.float64, device=f"cuda:{local}")
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def cpu_baseline(H, k, args):
+    """The C oracle (oracle/spa_oracle.c, OpenMP over frames) on a bounded
+    sample of the same workload; frames from the oracle's restatement of the
+    device frame source."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle
+    threads = args.cpu_threads or min(16, os.cpu_count() or 1)
+    sigma = oracle.sigma_for_snr(args.snr)
+    per = max(2 * threads, 16)
+    done, iters, t0 = 0, 0, time.perf_counter()
+    batch = 0
+    while True:
+        _, _, llr = oracle.generate_frames(H, SEED, 0, sigma, batch * per, per)
+        r = oracle.spa_decode(H, llr, args.iters, want_L=False, threads=threads)
+        done += per
+        iters += int(r["iters"].sum())
+        batch += 1
+        if time.perf_counter() - t0 >= args.cpu_seconds:
+            break
+    dt = time.perf_counter() - t0
+    return {"value": done / dt, "unit": "codewords/s", "cores": threads, "kind": "port",
+            "sample": f"{done} frames of {args.code}, T={args.iters}, snr={args.snr} dB "
+                      f"({iters} frame-iterations) in {dt:.1f} s; oracle/spa_oracle.c -O2 OpenMP",
+            "info_bits_per_s": done * k / dt}
+
+
+def main():
+    args = parse()
+    world, rank, local, dist = dist_setup(args)
+    if args.gpus != world and world > 1:
+        print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
+    import ldpc_amd
+    from ldpc_amd.device import Decoder, Graph
+
+    if ldpc_amd.device_count() <= 0:
+        raise SystemExit("bench.py: no HIP device visible (the decoder has no CPU path)")
+    edd = ldpc_amd.load_committed_code(args.code)
+    H = edd._h_std
+    n, m, k, nnz = edd._n, edd._m, edd._k, H.nnz
+    graph = Graph(H, device=local)
+    chunk = args.chunk or args.frames
+    dec = Decoder(graph, chunk)
+    sigma = 1.0 / math.sqrt(2.0 * 1.0 * (10.0 ** (args.snr * 0.1)))  # channel.py:113
+    B = args.frames
+
+    def step(s):
+        frame0 = (s * world + rank) * B
+        c = dec.mc_run(SEED, [sigma], B, frame0, args.iters)
+        return allreduce_counters(dist, c, local)
+
+    for s in range(args.warmup):
+        step(s)
+    barrier(dist, local)
+    dec.profile_read()  # drop anything recorded so far
+    dec.profile(True)
+    barrier(dist, local)
+    t0 = time.perf_counter()
+    totals = np.zeros((1, 7), np.int64)
+    for s in range(args.steps):
+        totals += step(args.warmup + s)
+    barrier(dist, local)
+    elapsed = time.perf_counter() - t0
+    dec.profile(False)
+    prof = dec.profile_read()
+    elapsed = max_over_ranks(dist, elapsed, local)
+
+    frames_total = int(totals[0, 0])
+    assert frames_total == B * world * args.steps, (frames_total, B, world, args.steps)
+    iters_total = int(totals[0, 6])  # whole job
+    cw_s = frames_total / elapsed
+
+    # roofline of the dominant kernel (cn_kernel) on THIS rank: algorithmic
+    # bytes = 16 B per edge per frame-iteration (read E_old + write E_new)
+    cn_ms, cn_launches = prof["cn"]
+    vn_ms, vn_launches = prof["vn"]
+    local_iters = iters_total // world  # frames per rank are statistically identical
+    cn_bytes_total = 16.0 * nnz * local_iters
+    cn_avg_s = (cn_ms / 1e3) / max(cn_launches, 1)
+    cn_bytes_per_launch = cn_bytes_total / max(cn_launches, 1)
+    achieved = cn_bytes_per_launch / cn_avg_s / 1e9 if cn_launches else 0.0
+    decode_ms = cn_ms + vn_ms
+    # whole-decode algorithmic bytes: 8n + sum_iters 16 E + ceil(n/8) + 8 per frame
+    frames_local = B * args.steps
+    dec_bytes = frames_local * (8 * n + math.ceil(n / 8) + 8) + 16.0 * nnz * local_iters
+    decode_gbs = dec_bytes / (decode_ms / 1e3) / 1e9 if decode_ms else 0.0
+
+    out = {
+        "metric": METRIC,
+        "value": cw_s,
+        "unit": "codewords/s",
+        "info_bits_per_s": cw_s * k,
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": elapsed / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic (on-device Philox4x32-10 info bits, [u, A.u] codewords, BPSK/AWGN, reference "
+                "channel model: noise std sigma^2, LLR 2y/sigma^2)",
+        "config": {
+            "workload": f"{args.code} SPA, max_iter {args.iters} + early termination, snr {args.snr} dB "
+                        f"(reference axis, speed 1), {B} frames/GPU/step",
+            "code": args.code, "n": n, "k": k, "edges_H_std": nnz, "max_iter": args.iters,
+            "snr_db": args.snr, "frames_per_gpu": B, "global_batch": B * world,
+            "parallelism": f"frame-sharded x{world}", "chunk_frames": chunk,
+        },
+        "fer": totals[0, 1] / frames_total,
+        "ber": totals[0, 2] / (k * frames_total),
+        "avg_iters": iters_total / frames_total,
+        "roofline": {
+            "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+            "kernel": "cn_kernel", "launches": cn_launches, "avg_launch_ms": cn_avg_s * 1e3,
+            "bytes_per_launch": cn_bytes_per_launch,
+            "bytes_model": "16 B x H_std edges x frame-iterations executed (E_old read + E_new write)",
+        },
+        "decode_roofline": {"achieved_GBs": decode_gbs, "frac": decode_gbs / HBM_PEAK_GBS,
+                            "cn_ms": cn_ms, "vn_ms": vn_ms, "gen_ms": prof["generate"][0],
+                            "count_ms": prof["count"][0]},
+        "cpu_baseline": None,
+    }
+    if rank == 0 and world == 1 and args.cpu_seconds > 0:
+        out["cpu_baseline"] = cpu_baseline(H, k, args)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,165 @@
+/*
+ * ldpc_hip.h -- C ABI of libldpc_hip.so, the MI355X (gfx950) SPA decoder.
+ *
+ * This is the drop-in boundary for the reference's hot path
+ * (python_ldpc_app/spa_decoder.py).  Plain C types only: pointers, sizes,
+ * int32/int64/double, and an opaque hipStream_t passed as void*.  The Python
+ * host (ldpc-simulator_amd/ldpc_amd/) binds it with ctypes; INTEGRATION.md
+ * shows the binding a maintainer of the reference would add.
+ *
+ * Conventions
+ *   - Every function returns 0 on success or a negative LDPC_E* code; the
+ *     message of the last failure on the calling thread is ldpc_last_error().
+ *   - Decoding failure is NOT an error: it is status 1 (Result.DATA_TRANSFER_NOT_OK),
+ *     exactly as spa_decoder.py:253 returns it.
+ *   - The caller owns every I/O buffer.  Without LDPC_F_DEVICE_PTRS the I/O
+ *     pointers are host memory and the call returns after the results are
+ *     copied back; with it they are device pointers on the decoder's GPU and
+ *     the call is asynchronous on `stream`.
+ *   - A graph is immutable after creation and may be shared read-only by
+ *     several decoders/threads.  A decoder (device workspace) is used by one
+ *     thread at a time, like the reference's SPA_Decoder instance (main.py:221).
+ *   - Frames are independent; a batch is split into chunks of at most the
+ *     decoder's capacity and each chunk runs all its iterations on the GPU.
+ */
+#ifndef LDPC_HIP_H
+#define LDPC_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define LDPC_ABI_VERSION 1
+
+/* error codes */
+#define LDPC_OK 0
+#define LDPC_EINVAL (-22)  /* bad argument / malformed matrix                   */
+#define LDPC_ENOMEM (-12)  /* host or device allocation failed                  */
+#define LDPC_EDEVICE (-5)  /* HIP runtime error (message in ldpc_last_error)    */
+#define LDPC_ERANGE (-34)  /* size does not fit the decoder / 32-bit indexing   */
+
+/* decode flags */
+#define LDPC_F_NLLR 0x1u        /* normalized-LLR metric, spa_decoder.py:210-228  */
+#define LDPC_F_DEVICE_PTRS 0x2u /* I/O pointers are device pointers, async        */
+
+typedef struct ldpc_hstd ldpc_hstd;       /* standard-form parity-check matrix  */
+typedef struct ldpc_graph ldpc_graph;     /* H_std uploaded to one GPU          */
+typedef struct ldpc_decoder ldpc_decoder; /* device workspace for one stream    */
+
+/* ---------------------------------------------------------------- misc */
+const char *ldpc_last_error(void);
+int ldpc_abi_version(void);
+/* number of visible GPUs (0 when none; never fails) */
+int ldpc_device_count(void);
+
+/* --------------------------------------------------- graph provider (host)
+ * Replaces EncoderDecoderData.create_standart_parity_check_matrix
+ * (encoder_decoder_data.py:269-317) and gaussian_elimination (:13-183):
+ * GF(2) Gauss-Jordan with the same pivot rule (first row >= cur_row with a 1,
+ * columns scanned 0..n-1), back-elimination, rank-deficient row drop (:280-305)
+ * and the column permutation [non-pivot cols ascending] + [pivot cols in pivot
+ * order] (:307-315).  Input: H (as read from the ALIST file, utils.py:21-113)
+ * in CSR, 0-based, any column order within a row; duplicate (row,col) entries
+ * are rejected with LDPC_EINVAL.
+ */
+int ldpc_hstd_build(int32_t m, int32_t n, const int32_t *row_ptr, const int32_t *col_idx,
+                    ldpc_hstd **out);
+/* Borrowed views valid until ldpc_hstd_free.  m_std = rank (rows kept). */
+int ldpc_hstd_get(const ldpc_hstd *h, int32_t *m_std, int32_t *n, int64_t *nnz,
+                  const int32_t **row_ptr, const int32_t **col_idx, const int32_t **perm);
+void ldpc_hstd_free(ldpc_hstd *h);
+
+/* ------------------------------------------------------------ graph (GPU)
+ * Replaces SPA_Decoder.__init__ (spa_decoder.py:16-42): binds H_std (CSR,
+ * ascending columns in every row -- the reference's check_to_var order) and
+ * builds the column view (var_to_check, rows ascending) on the device of the
+ * calling thread's current HIP device (`device` >= 0 selects one explicitly).
+ * k = n - m information bits sit in columns 0..k-1 (H_std = [A | I_m]).
+ */
+int ldpc_graph_create(int32_t m, int32_t n, const int32_t *row_ptr, const int32_t *col_idx,
+                      int32_t device, ldpc_graph **out);
+int ldpc_graph_destroy(ldpc_graph *g);
+int ldpc_graph_info(const ldpc_graph *g, int32_t *m, int32_t *n, int64_t *nnz,
+                    int32_t *max_row_deg, int32_t *max_col_deg);
+
+/* ---------------------------------------------------------- decoder
+ * Device workspace for chunks of up to `max_frames` frames (rounded up to a
+ * multiple of 64): fp64 messages E[tile][edge][64 frames], posteriors and
+ * channel LLRs [tile][col][64], per-frame state.  Bytes needed:
+ * ldpc_decoder_bytes().
+ */
+int64_t ldpc_decoder_bytes(const ldpc_graph *g, int32_t max_frames);
+int ldpc_decoder_create(const ldpc_graph *g, int32_t max_frames, ldpc_decoder **out);
+int ldpc_decoder_destroy(ldpc_decoder *d);
+int32_t ldpc_decoder_capacity(const ldpc_decoder *d);
+
+/*
+ * Batched SPA decode, fp64, results equal to spa_decoder.py:63-280 per frame.
+ * Replaces SPA_Decoder.decode(data_buffer) for `batch` frames at once.
+ *   llr          [batch][n]  channel LLRs in H_std column order (data_buffer._channel_data)
+ *   max_iter     >= 1        settings.get_max_iterations()
+ *   z_out        [batch][n]  hard output z (= data_buffer._decoded_data), uint8, or NULL
+ *   conv_out     [batch]     convergence_iteration (-1 if not converged) or NULL
+ *   status_out   [batch]     0 = Result.OK, 1 = Result.DATA_TRANSFER_NOT_OK, or NULL
+ *   post_out     [batch][n]  final a-posteriori LLRs, or NULL
+ *   nllr_out     [batch]     _d_summarize_normalized_llr (needs LDPC_F_NLLR), or NULL
+ *   nllr_hist    [batch][max_iter] per-iteration normalized LLR
+ *                            (_normalized_llr_by_iterations; unused tail = -1), or NULL
+ *   iters_out    [batch]     iterations executed (conv+1, or max_iter), or NULL
+ *   msg_out      [batch][nnz] final check->variable messages E in H_std CSR
+ *                            edge order (debug/parity; host memory only), or NULL
+ *   stream       hipStream_t or NULL (null stream)
+ */
+int ldpc_decode_f64(ldpc_decoder *d, int32_t batch, const double *llr, int32_t max_iter,
+                    uint32_t flags, uint8_t *z_out, int32_t *conv_out, int32_t *status_out,
+                    double *post_out, double *nllr_out, double *nllr_hist, int32_t *iters_out,
+                    double *msg_out, void *stream);
+
+/* ------------------------------------------- on-device Monte-Carlo frames
+ * Synthetic frame source that replaces DataBuffer(k) + encode + Channel
+ * mode 1 (data_buffer.py:16-82, channel.py:38-81, generator.py:7-9) on the GPU:
+ *   u  ~ iid bits from Philox4x32-10, key (seed), counter (frame, snr_point, block, 0)
+ *   c  = [u, A.u mod 2]  (H_std = [A | I_m])
+ *   x  = BPSK, bit 0 -> -1, bit 1 -> +1          (channel.py:49)
+ *   y  = x + sigma^2 * g,  g ~ N(0,1) Box-Muller  (channel.py:68-76: noise std is sigma^2)
+ *   llr = 2 y / sigma^2                           (channel.py:80)
+ * sigma = 1/sqrt(2*speed*10^(snr/10)) is computed by the caller (channel.py:113).
+ * ldpc_generate_frames writes them to host/device arrays (testing);
+ * ldpc_mc_run generates, decodes and reduces counters without leaving the GPU.
+ */
+int ldpc_generate_frames(ldpc_decoder *d, uint64_t seed, int32_t snr_point, double sigma,
+                         int64_t frame0, int32_t count, uint32_t flags, uint8_t *u_out,
+                         double *llr_out, void *stream);
+
+/* Counter vector per SNR point, int64[LDPC_MC_NCOUNT] (main.py:130-175 semantics):
+ *   [0] frames  [1] failed (Result != OK)  [2] error bits in failed frames' info part
+ *   [3] sum of convergence_iteration over converged frames  [4] converged frames
+ *   [5] sum over frames of the final normalized-LLR count (nllr = count/k)
+ *   [6] iterations executed (for roofline byte accounting)
+ */
+#define LDPC_MC_NCOUNT 7
+int ldpc_mc_run(ldpc_decoder *d, uint64_t seed, int32_t n_points, const double *sigmas,
+                int64_t frames_per_point, int64_t frame0, int32_t max_iter, uint32_t flags,
+                int64_t *counters_out, void *stream);
+
+/* ------------------------------------------------------------ profiling
+ * HIP-event timing of the decoder's own launches, on the stream they are
+ * launched on (used by bench.py for the live roofline).  While enabled, every
+ * kernel launch of this decoder is bracketed by events; ldpc_profile_read
+ * synchronises, returns the summed milliseconds and launch counts per kind
+ * (LDPC_K_*), and resets the accumulators.
+ */
+#define LDPC_K_CN 0
+#define LDPC_K_VN 1
+#define LDPC_K_GEN 2
+#define LDPC_K_COUNT 3
+#define LDPC_K_NKINDS 4
+int ldpc_profile_enable(ldpc_decoder *d, int enable);
+int ldpc_profile_read(ldpc_decoder *d, double *ms_out, int64_t *launches_out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* LDPC_HIP_H */

@@ -1,0 +1,591 @@
+// ldpc_api.cpp -- the C ABI of libldpc_hip.so (include/ldpc_hip.h).
+//
+// Host orchestration only: argument checks, device allocation, chunking of a
+// batch into frame tiles that fit the workspace, and the per-iteration launch
+// sequence (spa_kernels.hip).  Nothing here computes a decode result on the
+// CPU: without a GPU every entry point fails with LDPC_EDEVICE.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "ldpc_internal.h"
+#include "spa_device.h"
+
+using ldpc::DevGraph;
+using ldpc::DevState;
+using ldpc::kTile;
+
+static thread_local std::string g_last_error;
+
+int ldpc_fail(int code, const char *fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    g_last_error = buf;
+    return code;
+}
+
+#define HIP_TRY(expr)                                                                          \
+    do {                                                                                       \
+        hipError_t _e = (expr);                                                                \
+        if (_e != hipSuccess)                                                                  \
+            return ldpc_fail(LDPC_EDEVICE, "%s failed: %s (%s:%d)", #expr, hipGetErrorString(_e), \
+                             __FILE__, __LINE__);                                              \
+    } while (0)
+
+struct ldpc_graph {
+    int device = 0;
+    DevGraph dg{};
+    std::vector<int> h_row_ptr, h_col_idx;
+    int *d_ints = nullptr;  // one allocation for all index arrays
+};
+
+struct ldpc_decoder {
+    const ldpc_graph *g = nullptr;
+    int cap_tiles = 0;
+    double *E = nullptr, *L = nullptr, *ch = nullptr;
+    int *ints = nullptr;  // done, conv, status, iters, nllr_cnt (cap frames each) + tile_active
+    uint32_t *ubits = nullptr;
+    // staging for host I/O
+    double *llr_stage = nullptr, *post_stage = nullptr;
+    uint8_t *z_stage = nullptr;
+    unsigned long long *counters = nullptr;
+    int counters_cap = 0;
+    DevState st{};
+    // profiling (ldpc_profile_*)
+    bool prof = false;
+    struct Span {
+        int kind;
+        hipEvent_t a, b;
+    };
+    std::vector<Span> spans;
+    std::vector<hipEvent_t> pool;
+};
+
+namespace {
+
+struct DeviceGuard {
+    int prev = -1;
+    explicit DeviceGuard(int dev) {
+        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+        if (dev >= 0 && dev != prev) (void)hipSetDevice(dev);
+    }
+    ~DeviceGuard() {
+        if (prev >= 0) (void)hipSetDevice(prev);
+    }
+};
+
+int require_gpu() {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0)
+        return ldpc_fail(LDPC_EDEVICE, "no HIP device visible: the SPA decoder runs only on the GPU");
+    return LDPC_OK;
+}
+
+template <class T>
+int dev_alloc(T **p, size_t count) {
+    *p = nullptr;
+    if (count == 0) return LDPC_OK;
+    hipError_t e = hipMalloc((void **)p, count * sizeof(T));
+    if (e != hipSuccess) {
+        *p = nullptr;
+        return ldpc_fail(LDPC_ENOMEM, "hipMalloc(%zu bytes) failed: %s", count * sizeof(T), hipGetErrorString(e));
+    }
+    return LDPC_OK;
+}
+
+void state_bind(ldpc_decoder *d, int ntiles, int count) {
+    const size_t cap = (size_t)d->cap_tiles * kTile;
+    DevState &s = d->st;
+    s.E = d->E;
+    s.L = d->L;
+    s.ch = d->ch;
+    s.done = d->ints;
+    s.conv = d->ints + cap;
+    s.status = d->ints + 2 * cap;
+    s.iters = d->ints + 3 * cap;
+    s.nllr_cnt = d->ints + 4 * cap;
+    s.tile_active = d->ints + 5 * cap;
+    s.ubits = d->ubits;
+    s.nllr_hist = nullptr;
+    s.hist_stride = 0;
+    s.ntiles = ntiles;
+    s.count = count;
+}
+
+hipEvent_t take_event(ldpc_decoder *d) {
+    if (!d->pool.empty()) {
+        hipEvent_t e = d->pool.back();
+        d->pool.pop_back();
+        return e;
+    }
+    hipEvent_t e = nullptr;
+    if (hipEventCreate(&e) != hipSuccess) return nullptr;
+    return e;
+}
+
+// Launch `fn` bracketed by events when profiling is on.
+template <class F>
+hipError_t timed(ldpc_decoder *d, int kind, hipStream_t s, F &&fn) {
+    if (!d->prof) return fn();
+    hipEvent_t a = take_event(d), b = take_event(d);
+    if (a) (void)hipEventRecord(a, s);
+    hipError_t e = fn();
+    if (b) (void)hipEventRecord(b, s);
+    if (a && b) d->spans.push_back({kind, a, b});
+    return e;
+}
+
+hipError_t run_iterations(ldpc_decoder *d, const DevGraph &G, const DevState &st, int max_iter, bool nllr,
+                          hipStream_t s) {
+    hipError_t e = hipSuccess;
+    for (int it = 0; it < max_iter && e == hipSuccess; ++it) {
+        e = timed(d, LDPC_K_CN, s, [&] { return ldpc::launch_cn(G, st, it, s); });
+        if (e == hipSuccess)
+            e = timed(d, LDPC_K_VN, s, [&] { return ldpc::launch_vn(G, st, it, max_iter, nllr, s); });
+    }
+    return e;
+}
+
+size_t workspace_bytes(const DevGraph &g, int cap_tiles) {
+    const size_t cap = (size_t)cap_tiles * kTile;
+    const size_t kw = (size_t)((g.k + 31) / 32);
+    size_t b = 0;
+    b += cap * (size_t)g.nnz * 8;      // E
+    b += 2 * cap * (size_t)g.n * 8;    // L, ch
+    b += (5 * cap + cap_tiles) * 4;    // per-frame ints + tile flags
+    b += cap * kw * 4;                 // ubits
+    b += 2 * cap * (size_t)g.n * 8;    // llr/post staging
+    b += cap * (size_t)g.n;            // z staging
+    return b;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char *ldpc_last_error(void) { return g_last_error.c_str(); }
+int ldpc_abi_version(void) { return LDPC_ABI_VERSION; }
+
+int ldpc_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+// ------------------------------------------------------------------ graph
+int ldpc_graph_create(int32_t m, int32_t n, const int32_t *row_ptr, const int32_t *col_idx, int32_t device,
+                      ldpc_graph **out) {
+    if (!out) return ldpc_fail(LDPC_EINVAL, "ldpc_graph_create: out is NULL");
+    *out = nullptr;
+    if (m <= 0 || n <= 0 || m > n || !row_ptr || !col_idx)
+        return ldpc_fail(LDPC_EINVAL, "ldpc_graph_create: bad shape m=%d n=%d", m, n);
+    if (row_ptr[0] != 0) return ldpc_fail(LDPC_EINVAL, "ldpc_graph_create: row_ptr[0] != 0");
+    const int64_t nnz = row_ptr[m];
+    // within-tile offsets are 32-bit: e*64 must fit
+    if (nnz <= 0 || nnz > (int64_t)(INT32_MAX / kTile) || (int64_t)n > (int64_t)(INT32_MAX / kTile))
+        return ldpc_fail(LDPC_ERANGE, "ldpc_graph_create: nnz=%lld outside 32-bit tile indexing", (long long)nnz);
+    int max_row = 0;
+    for (int r = 0; r < m; ++r) {
+        const int b = row_ptr[r], e = row_ptr[r + 1];
+        if (e < b) return ldpc_fail(LDPC_EINVAL, "ldpc_graph_create: row_ptr not monotone at %d", r);
+        max_row = std::max(max_row, e - b);
+        for (int i = b; i < e; ++i) {
+            if (col_idx[i] < 0 || col_idx[i] >= n)
+                return ldpc_fail(LDPC_EINVAL, "ldpc_graph_create: column %d out of range", col_idx[i]);
+            if (i > b && col_idx[i] <= col_idx[i - 1])
+                return ldpc_fail(LDPC_EINVAL,
+                                 "ldpc_graph_create: row %d columns not strictly ascending "
+                                 "(the reference's check_to_var order is required)",
+                                 r);
+        }
+    }
+    if (int rc = require_gpu()) return rc;
+    auto *g = new ldpc_graph;
+    g->h_row_ptr.assign(row_ptr, row_ptr + m + 1);
+    g->h_col_idx.assign(col_idx, col_idx + nnz);
+    // CSC view with rows ascending (var_to_check order; also the order scipy's
+    // E.tocsc() sums a column in, spa_decoder.py:177-182)
+    std::vector<int> csc_ptr(n + 1, 0), csc_edge(nnz), csc_row(nnz);
+    for (int64_t e = 0; e < nnz; ++e) csc_ptr[col_idx[e] + 1]++;
+    for (int j = 0; j < n; ++j) csc_ptr[j + 1] += csc_ptr[j];
+    std::vector<int> fill(csc_ptr.begin(), csc_ptr.end() - 1);
+    int max_col = 0;
+    for (int j = 0; j < n; ++j) max_col = std::max(max_col, csc_ptr[j + 1] - csc_ptr[j]);
+    for (int r = 0; r < m; ++r)
+        for (int e = row_ptr[r]; e < row_ptr[r + 1]; ++e) {
+            const int p = fill[col_idx[e]]++;
+            csc_edge[p] = e;
+            csc_row[p] = r;
+        }
+    const int k = n - m;
+    // standard form check: row r's only column >= k is k+r (encoder needs it)
+    int std_form = 1;
+    for (int r = 0; r < m && std_form; ++r) {
+        int hits = 0;
+        for (int e = row_ptr[r]; e < row_ptr[r + 1]; ++e)
+            if (col_idx[e] >= k) hits += (col_idx[e] == k + r) ? 1 : 100;
+        std_form = hits == 1;
+    }
+    g->device = device;
+    DeviceGuard dg(device);
+    if (device < 0) (void)hipGetDevice(&g->device);
+    const size_t nints = (size_t)(m + 1) + nnz + (size_t)(n + 1) + 2 * (size_t)nnz;
+    if (int rc = dev_alloc(&g->d_ints, nints)) {
+        delete g;
+        return rc;
+    }
+    int *p = g->d_ints;
+    DevGraph &G = g->dg;
+    G.m = m;
+    G.n = n;
+    G.k = k;
+    G.nnz = (int)nnz;
+    G.max_row_deg = max_row;
+    G.max_col_deg = max_col;
+    G.std_form = std_form;
+    G.row_ptr = p;
+    p += m + 1;
+    G.col_idx = p;
+    p += nnz;
+    G.csc_ptr = p;
+    p += n + 1;
+    G.csc_edge = p;
+    p += nnz;
+    G.csc_row = p;
+    hipError_t e = hipSuccess;
+    if (e == hipSuccess) e = hipMemcpy((void *)G.row_ptr, row_ptr, sizeof(int) * (m + 1), hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy((void *)G.col_idx, col_idx, sizeof(int) * nnz, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy((void *)G.csc_ptr, csc_ptr.data(), sizeof(int) * (n + 1), hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy((void *)G.csc_edge, csc_edge.data(), sizeof(int) * nnz, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy((void *)G.csc_row, csc_row.data(), sizeof(int) * nnz, hipMemcpyHostToDevice);
+    if (e != hipSuccess) {
+        (void)hipFree(g->d_ints);
+        delete g;
+        return ldpc_fail(LDPC_EDEVICE, "ldpc_graph_create: upload failed: %s", hipGetErrorString(e));
+    }
+    *out = g;
+    return LDPC_OK;
+}
+
+int ldpc_graph_destroy(ldpc_graph *g) {
+    if (!g) return LDPC_OK;
+    DeviceGuard dg(g->device);
+    (void)hipFree(g->d_ints);
+    delete g;
+    return LDPC_OK;
+}
+
+int ldpc_graph_info(const ldpc_graph *g, int32_t *m, int32_t *n, int64_t *nnz, int32_t *max_row_deg,
+                    int32_t *max_col_deg) {
+    if (!g) return ldpc_fail(LDPC_EINVAL, "ldpc_graph_info: NULL graph");
+    if (m) *m = g->dg.m;
+    if (n) *n = g->dg.n;
+    if (nnz) *nnz = g->dg.nnz;
+    if (max_row_deg) *max_row_deg = g->dg.max_row_deg;
+    if (max_col_deg) *max_col_deg = g->dg.max_col_deg;
+    return LDPC_OK;
+}
+
+// ---------------------------------------------------------------- decoder
+int64_t ldpc_decoder_bytes(const ldpc_graph *g, int32_t max_frames) {
+    if (!g || max_frames <= 0) return -1;
+    const int tiles = (max_frames + kTile - 1) / kTile;
+    return (int64_t)workspace_bytes(g->dg, tiles);
+}
+
+int ldpc_decoder_create(const ldpc_graph *g, int32_t max_frames, ldpc_decoder **out) {
+    if (!out) return ldpc_fail(LDPC_EINVAL, "ldpc_decoder_create: out is NULL");
+    *out = nullptr;
+    if (!g || max_frames <= 0) return ldpc_fail(LDPC_EINVAL, "ldpc_decoder_create: bad arguments");
+    DeviceGuard dg(g->device);
+    auto *d = new ldpc_decoder;
+    d->g = g;
+    d->cap_tiles = (max_frames + kTile - 1) / kTile;
+    const size_t cap = (size_t)d->cap_tiles * kTile;
+    const DevGraph &G = g->dg;
+    const size_t kw = (size_t)((G.k + 31) / 32);
+    int rc = LDPC_OK;
+    if (!rc) rc = dev_alloc(&d->E, cap * (size_t)G.nnz);
+    if (!rc) rc = dev_alloc(&d->L, cap * (size_t)G.n);
+    if (!rc) rc = dev_alloc(&d->ch, cap * (size_t)G.n);
+    if (!rc) rc = dev_alloc(&d->ints, 5 * cap + (size_t)d->cap_tiles);
+    if (!rc) rc = dev_alloc(&d->ubits, std::max<size_t>(cap * kw, 1));
+    if (!rc) rc = dev_alloc(&d->llr_stage, cap * (size_t)G.n);
+    if (!rc) rc = dev_alloc(&d->post_stage, cap * (size_t)G.n);
+    if (!rc) rc = dev_alloc(&d->z_stage, cap * (size_t)G.n);
+    if (rc) {
+        ldpc_decoder_destroy(d);
+        return rc;
+    }
+    *out = d;
+    return LDPC_OK;
+}
+
+int ldpc_decoder_destroy(ldpc_decoder *d) {
+    if (!d) return LDPC_OK;
+    DeviceGuard dg(d->g ? d->g->device : -1);
+    (void)hipFree(d->E);
+    (void)hipFree(d->L);
+    (void)hipFree(d->ch);
+    (void)hipFree(d->ints);
+    (void)hipFree(d->ubits);
+    (void)hipFree(d->llr_stage);
+    (void)hipFree(d->post_stage);
+    (void)hipFree(d->z_stage);
+    (void)hipFree(d->counters);
+    for (auto &sp : d->spans) {
+        (void)hipEventDestroy(sp.a);
+        (void)hipEventDestroy(sp.b);
+    }
+    for (auto e : d->pool) (void)hipEventDestroy(e);
+    delete d;
+    return LDPC_OK;
+}
+
+int32_t ldpc_decoder_capacity(const ldpc_decoder *d) { return d ? d->cap_tiles * kTile : 0; }
+
+// ----------------------------------------------------------------- decode
+int ldpc_decode_f64(ldpc_decoder *d, int32_t batch, const double *llr, int32_t max_iter, uint32_t flags,
+                    uint8_t *z_out, int32_t *conv_out, int32_t *status_out, double *post_out, double *nllr_out,
+                    double *nllr_hist, int32_t *iters_out, double *msg_out, void *stream) {
+    if (!d) return ldpc_fail(LDPC_EINVAL, "ldpc_decode_f64: NULL decoder");
+    if (batch < 0) return ldpc_fail(LDPC_EINVAL, "ldpc_decode_f64: batch < 0");
+    if (max_iter < 1)
+        return ldpc_fail(LDPC_EINVAL,
+                         "ldpc_decode_f64: max_iter=%d; must be >= 1 (the reference loops until the "
+                         "syndrome clears for T<1, spa_decoder.py:104)",
+                         max_iter);
+    if (batch == 0) return LDPC_OK;
+    if (!llr) return ldpc_fail(LDPC_EINVAL, "ldpc_decode_f64: llr is NULL");
+    const bool dev_ptrs = flags & LDPC_F_DEVICE_PTRS;
+    const bool nllr = flags & LDPC_F_NLLR;
+    if (dev_ptrs && msg_out) return ldpc_fail(LDPC_EINVAL, "ldpc_decode_f64: msg_out is host-only");
+    DeviceGuard dg(d->g->device);
+    hipStream_t s = (hipStream_t)stream;
+    const DevGraph &G = d->g->dg;
+    const int n = G.n;
+    const int cap = d->cap_tiles * kTile;
+
+    double *d_hist = nullptr;
+    double *d_msgs = nullptr;
+    std::vector<int> h_ints;
+    std::vector<double> h_dbl;
+    int rc = LDPC_OK;
+    if (nllr_hist) {
+        if ((rc = dev_alloc(&d_hist, (size_t)cap * max_iter))) return rc;
+    }
+    if (msg_out) {
+        if ((rc = dev_alloc(&d_msgs, (size_t)cap * G.nnz))) {
+            (void)hipFree(d_hist);
+            return rc;
+        }
+    }
+    auto fail_dev = [&](hipError_t e, const char *what) {
+        (void)hipFree(d_hist);
+        (void)hipFree(d_msgs);
+        return ldpc_fail(LDPC_EDEVICE, "ldpc_decode_f64: %s: %s", what, hipGetErrorString(e));
+    };
+    hipError_t e = hipSuccess;
+    for (int start = 0; start < batch; start += cap) {
+        const int cnt = std::min(cap, batch - start);
+        const int ntiles = (cnt + kTile - 1) / kTile;
+        state_bind(d, ntiles, cnt);
+        DevState st = d->st;
+        if (d_hist) {
+            st.nllr_hist = d_hist;
+            st.hist_stride = max_iter;
+            if ((e = hipMemsetD8Async((hipDeviceptr_t)d_hist, 0xFF, sizeof(double) * (size_t)cnt * max_iter, s)))
+                return fail_dev(e, "memset");
+        }
+        const double *src = llr + (size_t)start * n;
+        if (!dev_ptrs) {
+            if ((e = hipMemcpyAsync(d->llr_stage, src, sizeof(double) * (size_t)cnt * n, hipMemcpyHostToDevice, s)))
+                return fail_dev(e, "llr upload");
+            src = d->llr_stage;
+        }
+        if ((e = ldpc::launch_reset(G, st, s))) return fail_dev(e, "reset");
+        if ((e = ldpc::launch_load_llr(G, st, src, s))) return fail_dev(e, "load");
+        if ((e = run_iterations(d, G, st, max_iter, nllr, s))) return fail_dev(e, "iteration");
+        uint8_t *zdst = dev_ptrs ? (z_out ? z_out + (size_t)start * n : nullptr) : d->z_stage;
+        double *pdst = dev_ptrs ? (post_out ? post_out + (size_t)start * n : nullptr) : (post_out ? d->post_stage : nullptr);
+        if (zdst || pdst) {
+            uint8_t *zz = zdst ? zdst : d->z_stage;
+            if ((e = ldpc::launch_finalize(G, st, zz, pdst, s))) return fail_dev(e, "finalize");
+        }
+        if (d_msgs && (e = ldpc::launch_export_msgs(G, st, d_msgs, s))) return fail_dev(e, "export");
+        // per-frame scalars
+        const size_t capz = (size_t)d->cap_tiles * kTile;
+        auto copy_ints = [&](int32_t *dst, const int *srcp) -> hipError_t {
+            if (!dst) return hipSuccess;
+            return hipMemcpyAsync(dst + start, srcp, sizeof(int) * cnt,
+                                  dev_ptrs ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost, s);
+        };
+        if ((e = copy_ints(conv_out, st.conv))) return fail_dev(e, "conv copy");
+        if ((e = copy_ints(status_out, st.status))) return fail_dev(e, "status copy");
+        if ((e = copy_ints(iters_out, st.iters))) return fail_dev(e, "iters copy");
+        (void)capz;
+        if (!dev_ptrs) {
+            if (z_out && (e = hipMemcpyAsync(z_out + (size_t)start * n, d->z_stage, (size_t)cnt * n,
+                                             hipMemcpyDeviceToHost, s)))
+                return fail_dev(e, "z copy");
+            if (post_out && (e = hipMemcpyAsync(post_out + (size_t)start * n, d->post_stage,
+                                                sizeof(double) * (size_t)cnt * n, hipMemcpyDeviceToHost, s)))
+                return fail_dev(e, "post copy");
+            if (msg_out && (e = hipMemcpyAsync(msg_out + (size_t)start * G.nnz, d_msgs,
+                                               sizeof(double) * (size_t)cnt * G.nnz, hipMemcpyDeviceToHost, s)))
+                return fail_dev(e, "msg copy");
+            if (nllr_hist && (e = hipMemcpyAsync(nllr_hist + (size_t)start * max_iter, d_hist,
+                                                 sizeof(double) * (size_t)cnt * max_iter, hipMemcpyDeviceToHost, s)))
+                return fail_dev(e, "hist copy");
+            if (nllr_out) {
+                h_ints.resize(cnt);
+                if ((e = hipMemcpyAsync(h_ints.data(), st.nllr_cnt, sizeof(int) * cnt, hipMemcpyDeviceToHost, s)))
+                    return fail_dev(e, "nllr copy");
+                if ((e = hipStreamSynchronize(s))) return fail_dev(e, "sync");
+                for (int i = 0; i < cnt; ++i)
+                    nllr_out[start + i] = nllr ? (G.k > 0 ? (double)h_ints[i] / G.k : 0.0) : 0.0;
+            }
+            // the staging buffers are reused by the next chunk
+            if ((e = hipStreamSynchronize(s))) return fail_dev(e, "sync");
+        } else if (nllr_out || nllr_hist) {
+            if (nllr_hist && (e = hipMemcpyAsync(nllr_hist + (size_t)start * max_iter, d_hist,
+                                                 sizeof(double) * (size_t)cnt * max_iter, hipMemcpyDeviceToDevice, s)))
+                return fail_dev(e, "hist copy");
+            if (nllr_out) {  // device path: convert counts on the host side of the stream
+                h_ints.resize(cnt);
+                h_dbl.resize(cnt);
+                if ((e = hipMemcpyAsync(h_ints.data(), st.nllr_cnt, sizeof(int) * cnt, hipMemcpyDeviceToHost, s)))
+                    return fail_dev(e, "nllr copy");
+                if ((e = hipStreamSynchronize(s))) return fail_dev(e, "sync");
+                for (int i = 0; i < cnt; ++i) h_dbl[i] = nllr ? (G.k > 0 ? (double)h_ints[i] / G.k : 0.0) : 0.0;
+                if ((e = hipMemcpy(nllr_out + start, h_dbl.data(), sizeof(double) * cnt, hipMemcpyHostToDevice)))
+                    return fail_dev(e, "nllr upload");
+            }
+        }
+    }
+    if (d_hist || d_msgs) {
+        if ((e = hipStreamSynchronize(s))) return fail_dev(e, "sync");
+    }
+    (void)hipFree(d_hist);
+    (void)hipFree(d_msgs);
+    if ((e = hipGetLastError())) return ldpc_fail(LDPC_EDEVICE, "ldpc_decode_f64: %s", hipGetErrorString(e));
+    return LDPC_OK;
+}
+
+// ------------------------------------------------------- Monte-Carlo path
+int ldpc_generate_frames(ldpc_decoder *d, uint64_t seed, int32_t snr_point, double sigma, int64_t frame0,
+                         int32_t count, uint32_t flags, uint8_t *u_out, double *llr_out, void *stream) {
+    if (!d) return ldpc_fail(LDPC_EINVAL, "ldpc_generate_frames: NULL decoder");
+    const DevGraph &G = d->g->dg;
+    if (!G.std_form) return ldpc_fail(LDPC_EINVAL, "ldpc_generate_frames: graph is not [A | I_m]");
+    if (count < 0 || count > d->cap_tiles * kTile || snr_point < 0 || frame0 < 0 || !(sigma > 0.0))
+        return ldpc_fail(LDPC_EINVAL, "ldpc_generate_frames: bad arguments (count=%d cap=%d)", count,
+                         d->cap_tiles * kTile);
+    if (count == 0) return LDPC_OK;
+    DeviceGuard dg(d->g->device);
+    hipStream_t s = (hipStream_t)stream;
+    const bool dev_ptrs = flags & LDPC_F_DEVICE_PTRS;
+    state_bind(d, (count + kTile - 1) / kTile, count);
+    uint8_t *u_dev = nullptr;
+    double *l_dev = nullptr;
+    int rc = LDPC_OK;
+    if (!dev_ptrs) {
+        if (u_out && (rc = dev_alloc(&u_dev, (size_t)count * G.k))) return rc;
+        l_dev = llr_out ? d->llr_stage : nullptr;
+    } else {
+        u_dev = u_out;
+        l_dev = llr_out;
+    }
+    HIP_TRY(ldpc::launch_generate(G, d->st, seed, snr_point, sigma, frame0, s));
+    // export writes u only for j<k, at [f][k]: give it the [count][k] buffer
+    HIP_TRY(ldpc::launch_export_frames(G, d->st, u_dev, l_dev, s));
+    if (!dev_ptrs) {
+        if (u_out) HIP_TRY(hipMemcpyAsync(u_out, u_dev, (size_t)count * G.k, hipMemcpyDeviceToHost, s));
+        if (llr_out)
+            HIP_TRY(hipMemcpyAsync(llr_out, l_dev, sizeof(double) * (size_t)count * G.n, hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipStreamSynchronize(s));
+        (void)hipFree(u_dev);
+    }
+    return LDPC_OK;
+}
+
+int ldpc_mc_run(ldpc_decoder *d, uint64_t seed, int32_t n_points, const double *sigmas, int64_t frames_per_point,
+                int64_t frame0, int32_t max_iter, uint32_t flags, int64_t *counters_out, void *stream) {
+    if (!d || n_points <= 0 || !sigmas || frames_per_point < 0 || frame0 < 0 || max_iter < 1 || !counters_out)
+        return ldpc_fail(LDPC_EINVAL, "ldpc_mc_run: bad arguments");
+    const DevGraph &G = d->g->dg;
+    if (!G.std_form) return ldpc_fail(LDPC_EINVAL, "ldpc_mc_run: graph is not [A | I_m]");
+    for (int p = 0; p < n_points; ++p)
+        if (!(sigmas[p] > 0.0)) return ldpc_fail(LDPC_EINVAL, "ldpc_mc_run: sigma[%d] <= 0", p);
+    DeviceGuard dg(d->g->device);
+    hipStream_t s = (hipStream_t)stream;
+    const bool nllr = flags & LDPC_F_NLLR;
+    const int need = n_points * LDPC_MC_NCOUNT;
+    if (d->counters_cap < need) {
+        (void)hipFree(d->counters);
+        d->counters = nullptr;
+        d->counters_cap = 0;
+        if (int rc = dev_alloc(&d->counters, (size_t)need)) return rc;
+        d->counters_cap = need;
+    }
+    HIP_TRY(hipMemsetAsync(d->counters, 0, sizeof(unsigned long long) * need, s));
+    const int64_t cap = (int64_t)d->cap_tiles * kTile;
+    for (int p = 0; p < n_points; ++p) {
+        for (int64_t start = 0; start < frames_per_point; start += cap) {
+            const int cnt = (int)std::min<int64_t>(cap, frames_per_point - start);
+            state_bind(d, (cnt + kTile - 1) / kTile, cnt);
+            HIP_TRY(ldpc::launch_reset(G, d->st, s));
+            const DevState st = d->st;
+            HIP_TRY(timed(d, LDPC_K_GEN, s,
+                          [&] { return ldpc::launch_generate(G, st, seed, p, sigmas[p], frame0 + start, s); }));
+            HIP_TRY(run_iterations(d, G, st, max_iter, nllr, s));
+            HIP_TRY(timed(d, LDPC_K_COUNT, s, [&] {
+                return ldpc::launch_count(G, st, d->counters + (size_t)p * LDPC_MC_NCOUNT, s);
+            }));
+        }
+    }
+    std::vector<unsigned long long> h(need);
+    HIP_TRY(hipMemcpyAsync(h.data(), d->counters, sizeof(unsigned long long) * need, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    for (int i = 0; i < need; ++i) counters_out[i] = (int64_t)h[i];
+    return LDPC_OK;
+}
+
+// -------------------------------------------------------------- profiling
+int ldpc_profile_enable(ldpc_decoder *d, int enable) {
+    if (!d) return ldpc_fail(LDPC_EINVAL, "ldpc_profile_enable: NULL decoder");
+    d->prof = enable != 0;
+    return LDPC_OK;
+}
+
+int ldpc_profile_read(ldpc_decoder *d, double *ms_out, int64_t *launches_out) {
+    if (!d) return ldpc_fail(LDPC_EINVAL, "ldpc_profile_read: NULL decoder");
+    DeviceGuard dg(d->g->device);
+    double ms[LDPC_K_NKINDS] = {0, 0, 0, 0};
+    int64_t cnt[LDPC_K_NKINDS] = {0, 0, 0, 0};
+    for (auto &sp : d->spans) {
+        HIP_TRY(hipEventSynchronize(sp.b));
+        float t = 0.f;
+        HIP_TRY(hipEventElapsedTime(&t, sp.a, sp.b));
+        ms[sp.kind] += t;
+        cnt[sp.kind] += 1;
+        d->pool.push_back(sp.a);
+        d->pool.push_back(sp.b);
+    }
+    d->spans.clear();
+    for (int i = 0; i < LDPC_K_NKINDS; ++i) {
+        if (ms_out) ms_out[i] = ms[i];
+        if (launches_out) launches_out[i] = cnt[i];
+    }
+    return LDPC_OK;
+}
+
+}  // extern "C"

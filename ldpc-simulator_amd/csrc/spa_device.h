@@ -1,0 +1,75 @@
+// spa_device.h -- device-side layout and kernel entry points of libldpc_hip.so.
+//
+// Data layout in HBM ("frame tiles"): 64 frames form one tile, one frame per
+// lane of a wavefront.  Every per-edge / per-column array is stored
+// [tile][item][64 lanes], so a wavefront touching item i of its tile reads
+// 64 consecutive doubles (512 contiguous bytes): fully coalesced, with no
+// index math per lane.
+//   E   [tile][nnz][64]  fp64 check->variable messages (CSR edge order of H_std)
+//   L   [tile][n][64]    fp64 a-posteriori LLRs
+//   ch  [tile][n][64]    fp64 channel LLRs
+//   ub  [tile][kw][64]   info bits (Monte-Carlo path), kw = ceil(k/32)
+// Per frame: done / conv / status / iters / nllr count; per tile: active flag.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <cstdint>
+
+namespace ldpc {
+
+constexpr int kTile = 64;  // frames per tile == wavefront width on CDNA
+
+struct DevGraph {
+    int m, n, k, nnz;
+    int max_row_deg, max_col_deg;
+    int std_form;            // 1 if H_std = [A | I_m] exactly (encoder usable)
+    const int *row_ptr;      // [m+1]
+    const int *col_idx;      // [nnz]
+    const int *csc_ptr;      // [n+1]
+    const int *csc_edge;     // [nnz] CSR edge id, rows ascending within a column
+    const int *csc_row;      // [nnz] row of that edge
+};
+
+struct DevState {
+    double *E, *L, *ch;
+    int *done, *conv, *status, *iters, *nllr_cnt;
+    int *tile_active;
+    uint32_t *ubits;         // MC only (may be null)
+    double *nllr_hist;       // [frame][hist_stride] or null
+    int hist_stride;
+    int ntiles;              // tiles in this chunk
+    int count;               // valid frames in this chunk
+};
+
+// --- launchers (spa_kernels.hip); all asynchronous on `s` ---
+hipError_t launch_reset(const DevGraph &g, const DevState &st, hipStream_t s);
+hipError_t launch_load_llr(const DevGraph &g, const DevState &st, const double *llr, hipStream_t s);
+hipError_t launch_cn(const DevGraph &g, const DevState &st, int it, hipStream_t s);
+hipError_t launch_vn(const DevGraph &g, const DevState &st, int it, int max_iter, bool nllr, hipStream_t s);
+hipError_t launch_finalize(const DevGraph &g, const DevState &st, uint8_t *z, double *post,
+                           hipStream_t s);
+hipError_t launch_export_msgs(const DevGraph &g, const DevState &st, double *out, hipStream_t s);
+hipError_t launch_generate(const DevGraph &g, const DevState &st, uint64_t seed, int snr_point,
+                           double sigma, int64_t frame0, hipStream_t s);
+hipError_t launch_export_frames(const DevGraph &g, const DevState &st, uint8_t *u_out, double *llr_out,
+                                hipStream_t s);
+hipError_t launch_count(const DevGraph &g, const DevState &st, unsigned long long *counters,
+                        hipStream_t s);
+
+// --- Philox4x32-10 (Salmon et al., SC'11), shared by host tests and device ---
+__host__ __device__ inline void philox4x32_10(uint32_t c[4], uint32_t k0, uint32_t k1) {
+#pragma unroll
+    for (int i = 0; i < 10; ++i) {
+        const uint64_t p0 = (uint64_t)0xD2511F53u * c[0];
+        const uint64_t p1 = (uint64_t)0xCD9E8D57u * c[2];
+        const uint32_t n0 = (uint32_t)(p1 >> 32) ^ c[1] ^ k0;
+        const uint32_t n2 = (uint32_t)(p0 >> 32) ^ c[3] ^ k1;
+        c[1] = (uint32_t)p1;
+        c[3] = (uint32_t)p0;
+        c[0] = n0;
+        c[2] = n2;
+        k0 += 0x9E3779B9u;
+        k1 += 0xBB67AE85u;
+    }
+}
+
+}  // namespace ldpc

@@ -1,0 +1,419 @@
+// spa_kernels.hip -- hand-written CDNA4 (gfx950) kernels of the SPA decoder.
+//
+// One decode iteration of python_ldpc_app/spa_decoder.py:104-276 is two
+// launches over a chunk of frame tiles (layout: spa_device.h):
+//
+//   cn_kernel  one wavefront per (tile, check row).  Lane = frame.  Walks the
+//              row's edges in ascending column order (the reference's
+//              check_to_var order) and reproduces spa_decoder.py:112-168 and
+//              the M update :260-268 fused in front of it:
+//                M = L[col] - E_old      (iteration 0: M = ch[col], :85-90)
+//                t = tanh(M/2) with the +-17.5 clip            (:138-146)
+//                P = t0*t1*...  strictly left to right          (np.prod, :152)
+//                q = P/t (|t|>1e-10) else prod of the others    (:159-164)
+//                E = 2*atanh(clip(q, +-CL))                     (:167-168)
+//              t is parked in E's slot between the two passes (same lane, same
+//              address), so the kernel needs no scratch.
+//   vn_kernel  one workgroup (16 wavefronts) per tile; wavefront w takes
+//              columns w, w+16, ...:
+//                L = ch + ((0+E[r0])+E[r1])+...  rows ascending (:173-185)
+//                z = L<0                                         (:188)
+//              and FUSES the early-termination syndrome (:191-204): every
+//              lane XORs its (z^1) into the m-bit row-parity vector of its
+//              frame held in LDS ([m/32][64] words, ds_xor_b32), then one
+//              wavefront ORs the words: zero -> converged at this iteration
+//              (:231-241), else NOT_OK at the last iteration (:244-253).
+//              The normalized-LLR count (:210-228) is fused here as well.
+//
+// Numerics: fp64 throughout; this file is compiled with -ffp-contract=off and
+// without fast-math, so every +,-,*,/ is one correctly rounded IEEE op in the
+// reference's order.  tanh/atanh come from the ROCm device library (<=1-2 ulp,
+// as numpy's own SVML/glibc versions are).
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdint>
+
+#include "spa_device.h"
+
+namespace ldpc {
+namespace {
+
+constexpr double kCL = 0.99999999999999878;  // spa_decoder.py:141,167
+constexpr double kTiny = 1e-10;              // spa_decoder.py:159
+constexpr int kCnRowsPerBlock = 4;           // 4 wavefronts = 4 rows of one tile
+constexpr int kVnWaves = 16;                 // wavefronts per VN workgroup
+
+__device__ __forceinline__ int uniform(int x) { return __builtin_amdgcn_readfirstlane(x); }
+
+__device__ __forceinline__ double clip_cl(double q) {
+    q = q < -kCL ? -kCL : q;  // np.clip keeps NaN, like these compares
+    return q > kCL ? kCL : q;
+}
+
+__device__ __forceinline__ double cn_tanh(double M) {
+    const double d = M * 0.5;  // == M/2.0 bit for bit (power-of-two scale)
+    return d > 17.5 ? kCL : (d < -17.5 ? -kCL : tanh(d));
+}
+
+// --------------------------------------------------------------- CN pass
+template <bool kFirst>
+__global__ __launch_bounds__(256) void cn_kernel(DevGraph g, DevState st, int blocks_per_tile) {
+    const int lane = threadIdx.x & 63;
+    const int wave = uniform(threadIdx.x >> 6);
+    // XCD-aware mapping: blocks b and b+8 share an XCD (round-robin dispatch),
+    // so give every block of one tile the same b%8: the tile's L/ch rows
+    // (gathered by every check row) then stay in that XCD's L2.
+    const int b = blockIdx.x;
+    const int slot = b >> 3;
+    const int tile = (slot / blocks_per_tile) * 8 + (b & 7);
+    const int row = (slot % blocks_per_tile) * kCnRowsPerBlock + wave;
+    if (tile >= st.ntiles || row >= g.m) return;
+    if (!st.tile_active[tile]) return;
+    const int beg = g.row_ptr[row], end = g.row_ptr[row + 1];
+    if (beg == end) return;  // spa_decoder.py:115-122
+
+    const int f = tile * kTile + lane;
+    const bool live = st.done[f] == 0;
+    double *Et = st.E + (size_t)tile * g.nnz * kTile + lane;
+    const double *Lt = (kFirst ? st.ch : st.L) + (size_t)tile * g.n * kTile + lane;
+
+    double P = 1.0;
+    for (int e = beg; e < end; ++e) {
+        const int c = g.col_idx[e];
+        double M = Lt[c * kTile];
+        if (!kFirst) M = M - Et[e * kTile];
+        const double t = cn_tanh(M);
+        P = (e == beg) ? t : P * t;
+        if (live) Et[e * kTile] = t;
+    }
+    for (int e = beg; e < end; ++e) {
+        const double t = Et[e * kTile];
+        double q;
+        if (fabs(t) > kTiny) {
+            q = P / t;
+        } else {  // np.prod(np.delete(tanh_array, idx)): rare, re-walk the row
+            q = 1.0;
+            bool first = true;
+            for (int e2 = beg; e2 < end; ++e2) {
+                if (e2 == e) continue;
+                const double t2 = Et[e2 * kTile];
+                q = first ? t2 : q * t2;
+                first = false;
+            }
+        }
+        const double En = 2.0 * atanh(clip_cl(q));
+        if (live) Et[e * kTile] = En;
+    }
+}
+
+// ------------------------------------------------------- VN + syndrome pass
+template <bool kFirst>
+__global__ __launch_bounds__(1024) void vn_kernel(DevGraph g, DevState st, int it, int last, int nllr) {
+    extern __shared__ uint32_t par[];  // [mw][64] row parities of z^1, one column per frame
+    __shared__ int cnt_lds[kTile];
+    const int tile = blockIdx.x;
+    if (!st.tile_active[tile]) return;
+    const int mw = (g.m + 31) >> 5;
+    for (int i = threadIdx.x; i < mw * kTile; i += blockDim.x) par[i] = 0u;
+    if (threadIdx.x < kTile) cnt_lds[threadIdx.x] = 0;
+    __syncthreads();
+
+    const int lane = threadIdx.x & 63;
+    const int wave = uniform(threadIdx.x >> 6);
+    const int nwaves = blockDim.x >> 6;
+    const int f = tile * kTile + lane;
+    const bool live = st.done[f] == 0;
+    const double *Et = st.E + (size_t)tile * g.nnz * kTile + lane;
+    double *Lt = st.L + (size_t)tile * g.n * kTile + lane;
+    const double *Ct = st.ch + (size_t)tile * g.n * kTile + lane;
+
+    int my_cnt = 0;
+    for (int j = wave; j < g.n; j += nwaves) {
+        const int p0 = g.csc_ptr[j], p1 = g.csc_ptr[j + 1];
+        double s = 0.0;  // scipy csr_matvec: sum starts at y[i] = 0
+        for (int p = p0; p < p1; ++p) s = s + Et[g.csc_edge[p] * kTile];
+        const double chj = Ct[j * kTile];
+        const double Lj = chj + s;  // channel added after the sum (:173,185)
+        if (nllr && j < g.k) {
+            const double ap = kFirst ? chj : Lt[j * kTile];  // a-priori = previous L (:274)
+            my_cnt += (fabs(Lj) <= 7.0 && ap * Lj < 0.0) ? 1 : 0;
+        }
+        if (live) Lt[j * kTile] = Lj;
+        if (!(Lj < 0.0)) {  // z^1 == 1 -> flips the parity of every row of column j
+            for (int p = p0; p < p1; ++p) {
+                const int r = g.csc_row[p];
+                atomicXor(&par[(r >> 5) * kTile + lane], 1u << (r & 31));
+            }
+        }
+    }
+    if (nllr) atomicAdd(&cnt_lds[lane], my_cnt);
+    __syncthreads();
+    if (wave != 0) return;
+
+    uint32_t acc = 0u;
+    for (int w = 0; w < mw; ++w) acc |= par[w * kTile + lane];
+    bool still = false;
+    if (live) {
+        if (nllr) {
+            const int c = cnt_lds[lane];
+            st.nllr_cnt[f] = c;
+            if (st.nllr_hist) st.nllr_hist[(size_t)f * st.hist_stride + it] = g.k > 0 ? (double)c / g.k : 0.0;
+        }
+        if (acc == 0u) {  // syndrome zero: Result.OK at this iteration
+            st.done[f] = 1;
+            st.conv[f] = it;
+            st.status[f] = 0;
+            st.iters[f] = it + 1;
+        } else if (last) {  // Result.DATA_TRANSFER_NOT_OK
+            st.done[f] = 1;
+            st.conv[f] = -1;
+            st.status[f] = 1;
+            st.iters[f] = it + 1;
+        } else {
+            still = true;
+        }
+    }
+    const unsigned long long any = __ballot(still);
+    if (lane == 0) st.tile_active[tile] = any != 0ull ? 1 : 0;
+}
+
+// ------------------------------------------------------------ plumbing kernels
+__global__ void reset_kernel(DevState st) {
+    const int f = blockIdx.x * blockDim.x + threadIdx.x;
+    if (f >= st.ntiles * kTile) return;
+    const bool valid = f < st.count;
+    st.done[f] = valid ? 0 : 1;
+    st.conv[f] = -1;
+    st.status[f] = 1;
+    st.iters[f] = 0;
+    st.nllr_cnt[f] = 0;
+    if ((f & 63) == 0) st.tile_active[f >> 6] = valid ? 1 : 0;
+}
+
+// llr [count][n] (row per frame) -> ch [tile][n][64]
+__global__ void load_llr_kernel(DevGraph g, DevState st, const double *llr) {
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const size_t total = (size_t)st.ntiles * g.n * kTile;
+    if (i >= total) return;
+    const int lane = (int)(i & 63);
+    const size_t tj = i >> 6;
+    const int j = (int)(tj % g.n);
+    const int tile = (int)(tj / g.n);
+    const int f = tile * kTile + lane;
+    st.ch[i] = f < st.count ? llr[(size_t)f * g.n + j] : 0.0;
+}
+
+// L [tile][n][64] -> z [count][n] (uint8, z = L<0) and optional post [count][n]
+__global__ void finalize_kernel(DevGraph g, DevState st, uint8_t *z, double *post) {
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const size_t total = (size_t)st.count * g.n;
+    if (i >= total) return;
+    const int f = (int)(i / g.n);
+    const int j = (int)(i % g.n);
+    const double L = st.L[((size_t)(f >> 6) * g.n + j) * kTile + (f & 63)];
+    z[i] = L < 0.0 ? 1 : 0;
+    if (post) post[i] = L;
+}
+
+__global__ void export_msgs_kernel(DevGraph g, DevState st, double *out) {
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const size_t total = (size_t)st.count * g.nnz;
+    if (i >= total) return;
+    const int f = (int)(i / g.nnz);
+    const int e = (int)(i % g.nnz);
+    out[i] = st.E[((size_t)(f >> 6) * g.nnz + e) * kTile + (f & 63)];
+}
+
+// ------------------------------------------------ on-device frame generation
+// One block of 64 threads per tile; thread = frame.  u bits live in LDS
+// ([kw][64], each lane reads only its own column, so no barrier is needed).
+__device__ __forceinline__ double u52(uint32_t hi, uint32_t lo) {
+    const uint64_t x = (((uint64_t)hi << 32) | lo) >> 12;  // 52 random bits
+    return ((double)x + 0.5) * 0x1p-52;                    // exact, in (0,1)
+}
+
+__global__ __launch_bounds__(64) void generate_kernel(DevGraph g, DevState st, uint64_t seed, int snr_point,
+                                                      double sigma, int64_t frame0) {
+    extern __shared__ uint32_t ul[];
+    const int tile = blockIdx.x;
+    const int lane = threadIdx.x;
+    const int f = tile * kTile + lane;
+    const int kw = (g.k + 31) >> 5;
+    const int64_t F = frame0 + f;
+    const uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
+    const uint32_t flo = (uint32_t)F, fhi = (uint32_t)((uint64_t)F >> 32);
+    // info bits: data_buffer.py:23 / generator.py:7-9 (random.randint(0,1) per bit)
+    for (int blk = 0; blk * 4 < kw; ++blk) {
+        uint32_t c[4] = {flo, fhi, (uint32_t)blk, (uint32_t)snr_point << 1};
+        philox4x32_10(c, k0, k1);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int w = blk * 4 + q;
+            if (w >= kw) break;
+            uint32_t v = c[q];
+            if (w == kw - 1 && (g.k & 31)) v &= (1u << (g.k & 31)) - 1u;
+            ul[w * kTile + lane] = v;
+            st.ubits[((size_t)tile * kw + w) * kTile + lane] = v;
+        }
+    }
+    // codeword [u, A.u mod 2] + BPSK + AWGN (channel.py:49,68-80)
+    const double s2 = sigma * sigma;
+    double *Ct = st.ch + (size_t)tile * g.n * kTile + lane;
+    for (int jb = 0; jb < g.n; jb += 2) {
+        uint32_t c[4] = {flo, fhi, (uint32_t)(jb >> 1), ((uint32_t)snr_point << 1) | 1u};
+        philox4x32_10(c, k0, k1);
+        const double u1 = u52(c[0], c[1]);
+        const double u2 = u52(c[2], c[3]);
+        const double r = sqrt(-2.0 * log(u1));
+        const double th = 6.283185307179586 * u2;
+        const double gz[2] = {r * cos(th), r * sin(th)};
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+            const int j = jb + q;
+            if (j >= g.n) break;
+            uint32_t bit;
+            if (j < g.k) {
+                bit = (ul[(j >> 5) * kTile + lane] >> (j & 31)) & 1u;
+            } else {  // parity bit of row j-k: XOR of u over A's columns of that row
+                const int rr = j - g.k;
+                bit = 0u;
+                for (int e = g.row_ptr[rr]; e < g.row_ptr[rr + 1]; ++e) {
+                    const int cc = g.col_idx[e];
+                    if (cc < g.k) bit ^= (ul[(cc >> 5) * kTile + lane] >> (cc & 31)) & 1u;
+                }
+            }
+            const double x = bit ? 1.0 : -1.0;
+            const double y = x + s2 * gz[q];
+            Ct[j * kTile] = f < st.count ? (2.0 * y) / s2 : 0.0;
+        }
+    }
+}
+
+__global__ void export_frames_kernel(DevGraph g, DevState st, uint8_t *u_out, double *llr_out) {
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const size_t total = (size_t)st.count * g.n;
+    if (i >= total) return;
+    const int f = (int)(i / g.n);
+    const int j = (int)(i % g.n);
+    const int tile = f >> 6, lane = f & 63;
+    if (llr_out) llr_out[i] = st.ch[((size_t)tile * g.n + j) * kTile + lane];
+    if (u_out && j < g.k) {
+        const int kw = (g.k + 31) >> 5;
+        const uint32_t w = st.ubits[((size_t)tile * kw + (j >> 5)) * kTile + lane];
+        u_out[(size_t)f * g.k + j] = (uint8_t)((w >> (j & 31)) & 1u);
+    }
+}
+
+__device__ __forceinline__ unsigned long long wave_sum(unsigned long long v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    return v;
+}
+
+// Per-frame Monte-Carlo counters (main.py:130-138 + :154-172), one wave per tile.
+__global__ __launch_bounds__(64) void count_kernel(DevGraph g, DevState st, unsigned long long *ctr) {
+    const int tile = blockIdx.x;
+    const int lane = threadIdx.x;
+    const int f = tile * kTile + lane;
+    const bool valid = f < st.count;
+    const int kw = (g.k + 31) >> 5;
+    unsigned long long v[7] = {0, 0, 0, 0, 0, 0, 0};
+    if (valid) {
+        const bool ok = st.status[f] == 0;
+        v[0] = 1;
+        v[1] = ok ? 0 : 1;
+        if (!ok) {  // BER counts only frames whose syndrome check failed (main.py:130-138)
+            const double *Lt = st.L + (size_t)tile * g.n * kTile + lane;
+            unsigned long long err = 0;
+            for (int w = 0; w < kw; ++w) {
+                const uint32_t u = st.ubits[((size_t)tile * kw + w) * kTile + lane];
+                uint32_t dec = 0u;
+                const int nb = min(32, g.k - w * 32);
+                for (int b = 0; b < nb; ++b)
+                    dec |= (Lt[(w * 32 + b) * kTile] < 0.0 ? 0u : 1u) << b;  // z^1
+                err += __popc(u ^ dec);
+            }
+            v[2] = err;
+        }
+        const int cv = st.conv[f];
+        v[3] = cv >= 0 ? (unsigned long long)cv : 0;
+        v[4] = cv >= 0 ? 1 : 0;
+        v[5] = (unsigned long long)st.nllr_cnt[f];
+        v[6] = (unsigned long long)st.iters[f];
+    }
+#pragma unroll
+    for (int i = 0; i < 7; ++i) {
+        const unsigned long long s = wave_sum(v[i]);
+        if (lane == 0 && s) atomicAdd(&ctr[i], s);
+    }
+}
+
+inline unsigned grid_for(size_t total, int block) { return (unsigned)((total + block - 1) / block); }
+
+}  // namespace
+
+hipError_t launch_reset(const DevGraph &, const DevState &st, hipStream_t s) {
+    const int total = st.ntiles * kTile;
+    reset_kernel<<<grid_for(total, 256), 256, 0, s>>>(st);
+    return hipGetLastError();
+}
+
+hipError_t launch_load_llr(const DevGraph &g, const DevState &st, const double *llr, hipStream_t s) {
+    const size_t total = (size_t)st.ntiles * g.n * kTile;
+    load_llr_kernel<<<grid_for(total, 256), 256, 0, s>>>(g, st, llr);
+    return hipGetLastError();
+}
+
+hipError_t launch_cn(const DevGraph &g, const DevState &st, int it, hipStream_t s) {
+    const int bpt = (g.m + kCnRowsPerBlock - 1) / kCnRowsPerBlock;
+    const unsigned grid = (unsigned)(((st.ntiles + 7) / 8) * 8 * bpt);
+    if (it == 0)
+        cn_kernel<true><<<grid, 256, 0, s>>>(g, st, bpt);
+    else
+        cn_kernel<false><<<grid, 256, 0, s>>>(g, st, bpt);
+    return hipGetLastError();
+}
+
+hipError_t launch_vn(const DevGraph &g, const DevState &st, int it, int max_iter, bool nllr, hipStream_t s) {
+    const size_t lds = (size_t)((g.m + 31) >> 5) * kTile * sizeof(uint32_t);
+    const int last = it == max_iter - 1 ? 1 : 0;
+    if (it == 0)
+        vn_kernel<true><<<st.ntiles, kVnWaves * 64, lds, s>>>(g, st, it, last, nllr ? 1 : 0);
+    else
+        vn_kernel<false><<<st.ntiles, kVnWaves * 64, lds, s>>>(g, st, it, last, nllr ? 1 : 0);
+    return hipGetLastError();
+}
+
+hipError_t launch_finalize(const DevGraph &g, const DevState &st, uint8_t *z, double *post, hipStream_t s) {
+    const size_t total = (size_t)st.count * g.n;
+    if (total) finalize_kernel<<<grid_for(total, 256), 256, 0, s>>>(g, st, z, post);
+    return hipGetLastError();
+}
+
+hipError_t launch_export_msgs(const DevGraph &g, const DevState &st, double *out, hipStream_t s) {
+    const size_t total = (size_t)st.count * g.nnz;
+    if (total) export_msgs_kernel<<<grid_for(total, 256), 256, 0, s>>>(g, st, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_generate(const DevGraph &g, const DevState &st, uint64_t seed, int snr_point, double sigma,
+                           int64_t frame0, hipStream_t s) {
+    const size_t lds = (size_t)((g.k + 31) >> 5) * kTile * sizeof(uint32_t);
+    generate_kernel<<<st.ntiles, kTile, lds, s>>>(g, st, seed, snr_point, sigma, frame0);
+    return hipGetLastError();
+}
+
+hipError_t launch_export_frames(const DevGraph &g, const DevState &st, uint8_t *u_out, double *llr_out,
+                                hipStream_t s) {
+    const size_t total = (size_t)st.count * g.n;
+    if (total) export_frames_kernel<<<grid_for(total, 256), 256, 0, s>>>(g, st, u_out, llr_out);
+    return hipGetLastError();
+}
+
+hipError_t launch_count(const DevGraph &g, const DevState &st, unsigned long long *counters, hipStream_t s) {
+    count_kernel<<<st.ntiles, kTile, 0, s>>>(g, st, counters);
+    return hipGetLastError();
+}
+
+}  // namespace ldpc

@@ -1,0 +1,118 @@
+"""ctypes binding of libldpc_hip.so (C ABI: include/ldpc_hip.h).
+
+The shared library is built in-tree (``ldpc-simulator_amd/csrc/Makefile`` ->
+``ldpc_amd/libldpc_hip.so``).  There is no fallback: if the library is
+missing, or a compute entry point is called without a GPU, this module raises.
+"""
+import ctypes
+import os
+import threading
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("LDPC_HIP_LIB", os.path.join(_HERE, "libldpc_hip.so"))
+
+LDPC_F_NLLR = 0x1
+LDPC_F_DEVICE_PTRS = 0x2
+LDPC_MC_NCOUNT = 7
+
+# every symbol include/ldpc_hip.h declares
+EXPORTED = (
+    "ldpc_last_error", "ldpc_abi_version", "ldpc_device_count",
+    "ldpc_hstd_build", "ldpc_hstd_get", "ldpc_hstd_free",
+    "ldpc_graph_create", "ldpc_graph_destroy", "ldpc_graph_info",
+    "ldpc_decoder_bytes", "ldpc_decoder_create", "ldpc_decoder_destroy", "ldpc_decoder_capacity",
+    "ldpc_decode_f64", "ldpc_generate_frames", "ldpc_mc_run",
+    "ldpc_profile_enable", "ldpc_profile_read",
+)
+
+
+class LdpcError(RuntimeError):
+    """A libldpc_hip.so call failed (the message is ldpc_last_error())."""
+
+    def __init__(self, fn, code, msg):
+        super().__init__(f"{fn} failed ({code}): {msg}")
+        self.code = code
+
+
+_lock = threading.Lock()
+_lib = None
+
+P = ctypes.POINTER
+c_i32, c_i64, c_u32, c_u64, c_dbl, c_vp = (ctypes.c_int32, ctypes.c_int64, ctypes.c_uint32,
+                                           ctypes.c_uint64, ctypes.c_double, ctypes.c_void_p)
+
+
+def _declare(lib):
+    sig = {
+        "ldpc_last_error": (ctypes.c_char_p, []),
+        "ldpc_abi_version": (ctypes.c_int, []),
+        "ldpc_device_count": (ctypes.c_int, []),
+        "ldpc_hstd_build": (ctypes.c_int, [c_i32, c_i32, P(c_i32), P(c_i32), P(c_vp)]),
+        "ldpc_hstd_get": (ctypes.c_int, [c_vp, P(c_i32), P(c_i32), P(c_i64), P(P(c_i32)),
+                                         P(P(c_i32)), P(P(c_i32))]),
+        "ldpc_hstd_free": (None, [c_vp]),
+        "ldpc_graph_create": (ctypes.c_int, [c_i32, c_i32, P(c_i32), P(c_i32), c_i32, P(c_vp)]),
+        "ldpc_graph_destroy": (ctypes.c_int, [c_vp]),
+        "ldpc_graph_info": (ctypes.c_int, [c_vp, P(c_i32), P(c_i32), P(c_i64), P(c_i32), P(c_i32)]),
+        "ldpc_decoder_bytes": (c_i64, [c_vp, c_i32]),
+        "ldpc_decoder_create": (ctypes.c_int, [c_vp, c_i32, P(c_vp)]),
+        "ldpc_decoder_destroy": (ctypes.c_int, [c_vp]),
+        "ldpc_decoder_capacity": (c_i32, [c_vp]),
+        "ldpc_decode_f64": (ctypes.c_int, [c_vp, c_i32, c_vp, c_i32, c_u32, c_vp, c_vp, c_vp, c_vp,
+                                           c_vp, c_vp, c_vp, c_vp, c_vp]),
+        "ldpc_generate_frames": (ctypes.c_int, [c_vp, c_u64, c_i32, c_dbl, c_i64, c_i32, c_u32,
+                                                c_vp, c_vp, c_vp]),
+        "ldpc_mc_run": (ctypes.c_int, [c_vp, c_u64, c_i32, P(c_dbl), c_i64, c_i64, c_i32, c_u32,
+                                       P(c_i64), c_vp]),
+        "ldpc_profile_enable": (ctypes.c_int, [c_vp, ctypes.c_int]),
+        "ldpc_profile_read": (ctypes.c_int, [c_vp, P(c_dbl), P(c_i64)]),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+
+
+def lib():
+    """Load (once) and return the ctypes handle; raises if the .so is absent."""
+    global _lib
+    with _lock:
+        if _lib is None:
+            if not os.path.exists(LIB_PATH):
+                raise ImportError(
+                    f"libldpc_hip.so not found at {LIB_PATH}: build it with "
+                    "`make -C ldpc-simulator_amd/csrc` (or __graft_entry__.build()). "
+                    "There is no CPU fallback.")
+            handle = ctypes.CDLL(LIB_PATH)
+            _declare(handle)
+            _lib = handle
+    return _lib
+
+
+def check(fn_name, rc):
+    if rc != 0:
+        msg = lib().ldpc_last_error()
+        raise LdpcError(fn_name, rc, msg.decode() if msg else "")
+    return rc
+
+
+def ptr(a):
+    """Address of a C-contiguous numpy array (or None -> NULL)."""
+    if a is None:
+        return None
+    assert a.flags["C_CONTIGUOUS"], "array must be C-contiguous"
+    return a.ctypes.data
+
+
+def i32p(a):
+    return a.ctypes.data_as(P(c_i32))
+
+
+def device_count():
+    return int(lib().ldpc_device_count())
+
+
+def as_i32(a):
+    return np.ascontiguousarray(np.asarray(a, dtype=np.int32))

@@ -1,0 +1,148 @@
+"""Python handles over the C ABI: the graph on a GPU and a decoder workspace.
+
+``Graph``   wraps ldpc_graph_create (H_std uploaded once per device, cached by
+            content so repeated SPA_Decoder constructions -- main.py:221 builds
+            one per SNR point, main.py:78 one per frame -- do not re-upload).
+``Decoder`` wraps ldpc_decoder_create / ldpc_decode_f64 / ldpc_mc_run.
+"""
+import ctypes
+import hashlib
+import threading
+
+import numpy as np
+from scipy import sparse
+
+from . import _lib
+from ._lib import LDPC_F_NLLR, LDPC_MC_NCOUNT, as_i32, check
+
+
+def _csr_arrays(H):
+    H = sparse.csr_matrix(H)
+    if not H.has_sorted_indices:
+        H = H.sorted_indices()
+    return H.shape[0], H.shape[1], as_i32(H.indptr), as_i32(H.indices)
+
+
+class Graph:
+    """H_std (CSR, ascending columns) resident on one GPU."""
+
+    _cache = {}
+    _cache_lock = threading.Lock()
+
+    def __init__(self, H, device=-1):
+        m, n, indptr, indices = _csr_arrays(H)
+        self.m, self.n, self.k = m, n, n - m
+        self.indptr, self.indices = indptr, indices
+        self.nnz = int(indptr[-1])
+        h = ctypes.c_void_p()
+        check("ldpc_graph_create", _lib.lib().ldpc_graph_create(
+            m, n, _lib.i32p(indptr), _lib.i32p(indices), int(device), ctypes.byref(h)))
+        self._h = h
+        mr, mc = ctypes.c_int32(), ctypes.c_int32()
+        check("ldpc_graph_info", _lib.lib().ldpc_graph_info(h, None, None, None, ctypes.byref(mr), ctypes.byref(mc)))
+        self.max_row_deg, self.max_col_deg = mr.value, mc.value
+
+    @property
+    def handle(self):
+        return self._h
+
+    @classmethod
+    def cached(cls, H, device=-1):
+        m, n, indptr, indices = _csr_arrays(H)
+        key = (m, n, int(device), hashlib.sha1(indptr.tobytes() + indices.tobytes()).hexdigest())
+        with cls._cache_lock:
+            g = cls._cache.get(key)
+            if g is None:
+                g = cls(sparse.csr_matrix((np.ones(len(indices), np.int32), indices, indptr), shape=(m, n)), device)
+                cls._cache[key] = g
+        return g
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h is not None and h.value and _lib._lib is not None:
+            _lib._lib.ldpc_graph_destroy(h)
+            self._h = None
+
+
+class DecodeResult(dict):
+    __getattr__ = dict.__getitem__
+
+
+class Decoder:
+    """Device workspace for chunks of up to `max_frames` frames."""
+
+    def __init__(self, graph, max_frames=4096):
+        self.graph = graph
+        h = ctypes.c_void_p()
+        check("ldpc_decoder_create", _lib.lib().ldpc_decoder_create(graph.handle, int(max_frames), ctypes.byref(h)))
+        self._h = h
+        self.capacity = int(_lib.lib().ldpc_decoder_capacity(h))
+
+    @staticmethod
+    def workspace_bytes(graph, max_frames):
+        return int(_lib.lib().ldpc_decoder_bytes(graph.handle, int(max_frames)))
+
+    def decode(self, llr, max_iter, nllr=False, post=False, hist=False, msgs=False):
+        """Decode [B, n] channel LLRs (H_std column order).  Returns numpy arrays."""
+        g = self.graph
+        llr = np.ascontiguousarray(np.asarray(llr, dtype=np.float64))
+        if llr.ndim == 1:
+            llr = llr[None, :]
+        if llr.ndim != 2 or llr.shape[1] != g.n:
+            raise ValueError(f"llr must be [batch, {g.n}], got {llr.shape}")
+        B = llr.shape[0]
+        T = int(max_iter)
+        z = np.empty((B, g.n), np.uint8)
+        conv = np.empty(B, np.int32)
+        status = np.empty(B, np.int32)
+        iters = np.empty(B, np.int32)
+        nl = np.zeros(B, np.float64) if nllr else None
+        Lp = np.empty((B, g.n), np.float64) if post else None
+        hi = np.empty((B, T), np.float64) if (hist and nllr) else None
+        E = np.empty((B, g.nnz), np.float64) if msgs else None
+        flags = LDPC_F_NLLR if nllr else 0
+        check("ldpc_decode_f64", _lib.lib().ldpc_decode_f64(
+            self._h, B, _lib.ptr(llr), T, flags, _lib.ptr(z), _lib.ptr(conv), _lib.ptr(status),
+            _lib.ptr(Lp), _lib.ptr(nl), _lib.ptr(hi), _lib.ptr(iters), _lib.ptr(E), None))
+        return DecodeResult(z=z, conv=conv, status=status, iters=iters, nllr=nl, post=Lp, hist=hi, msgs=E)
+
+    def generate(self, seed, snr_point, sigma, frame0, count):
+        """On-device synthetic frames (u bits, channel LLRs) copied back for testing."""
+        g = self.graph
+        u = np.empty((count, g.k), np.uint8)
+        llr = np.empty((count, g.n), np.float64)
+        check("ldpc_generate_frames", _lib.lib().ldpc_generate_frames(
+            self._h, int(seed), int(snr_point), float(sigma), int(frame0), int(count), 0,
+            _lib.ptr(u), _lib.ptr(llr), None))
+        return u, llr
+
+    def mc_run(self, seed, sigmas, frames_per_point, frame0, max_iter, nllr=False):
+        """Generate + decode + count on the GPU; returns int64 [n_points, 7] counters."""
+        sig = np.ascontiguousarray(np.asarray(sigmas, dtype=np.float64))
+        out = np.zeros((len(sig), LDPC_MC_NCOUNT), np.int64)
+        check("ldpc_mc_run", _lib.lib().ldpc_mc_run(
+            self._h, int(seed), len(sig), sig.ctypes.data_as(ctypes.POINTER(ctypes.c_double)),
+            int(frames_per_point), int(frame0), int(max_iter), LDPC_F_NLLR if nllr else 0,
+            out.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)), None))
+        return out
+
+    KINDS = ("cn", "vn", "generate", "count")
+
+    def profile(self, enable=True):
+        check("ldpc_profile_enable", _lib.lib().ldpc_profile_enable(self._h, 1 if enable else 0))
+
+    def profile_read(self):
+        """{kind: (total_ms, launches)} of this decoder's launches since the last read."""
+        ms = (ctypes.c_double * 4)()
+        n = (ctypes.c_int64 * 4)()
+        check("ldpc_profile_read", _lib.lib().ldpc_profile_read(self._h, ms, n))
+        return {k: (ms[i], n[i]) for i, k in enumerate(self.KINDS)}
+
+    def close(self):
+        h = getattr(self, "_h", None)
+        if h is not None and h.value and _lib._lib is not None:
+            _lib._lib.ldpc_decoder_destroy(h)
+        self._h = None
+
+    def __del__(self):
+        self.close()

@@ -1,0 +1,80 @@
+"""Drop-in SPA_Decoder backed by the HIP kernels (libldpc_hip.so).
+
+Same constructor and call as python_ldpc_app/spa_decoder.py:
+    SPA_Decoder(encoder_decoder_data, settings)            (:16-42)
+    decode(data_buffer) -> Result                          (:63-280)
+reads data_buffer._channel_data, writes data_buffer._decoded_data (the hard
+output z, the complement of the bit estimate), and sets convergence_iteration,
+_normalized_llr_by_iterations (appended per iteration, never reset -- :19-22,
+:226-228) and _d_summarize_normalized_llr.  Failure to converge is
+Result.DATA_TRANSFER_NOT_OK, not an exception; bad arguments raise.
+
+`encoder_decoder_data` may be ours (ldpc_amd.code.EncoderDecoderData) or the
+reference's: only `_h_sparse_cached` (else `_h_std`), `_m` and `_n` are read,
+as the reference does.  `decode_batch` decodes many frames per launch.
+"""
+import numpy as np
+from scipy import sparse
+
+from .device import Decoder, Graph
+from .enums import caller_result_enum
+
+
+def _graph_matrix(edd):
+    H = getattr(edd, "_h_sparse_cached", None)
+    if H is None:
+        H = edd._h_std
+        H = H.get_sparse_matrix() if hasattr(H, "get_sparse_matrix") else H
+    return sparse.csr_matrix(H)
+
+
+class SPA_Decoder:
+    def __init__(self, encoder_decoder_data, settings, device=-1, max_frames=64):
+        self.m_pData = encoder_decoder_data
+        self.m_pSettings = settings
+        self._arr_changed_by_iterations = []
+        self._normalized_llr_by_iterations = []
+        self._normalized_llr_by_iterations_soft = []
+        self._d_summarize_normalized_llr = 0.0
+        self._arr_aposteriori_llrs = []
+        self.convergence_iteration = -1
+        H = _graph_matrix(encoder_decoder_data)
+        if H.shape != (encoder_decoder_data._m, encoder_decoder_data._n):
+            raise ValueError(f"H_std shape {H.shape} != (m, n) = "
+                             f"({encoder_decoder_data._m}, {encoder_decoder_data._n})")
+        self.H_sparse = H
+        self._graph = Graph.cached(H, device)
+        self._dev = Decoder(self._graph, max_frames)
+        self._Result = caller_result_enum()
+
+    # ------------------------------------------------------------ one frame
+    def decode(self, p_data_buffer):
+        T = int(self.m_pSettings.get_max_iterations())
+        nllr = bool(self.m_pSettings.is_normalized_llr_calculate())
+        ch = np.asarray(p_data_buffer._channel_data, dtype=np.float64)
+        r = self._dev.decode(ch[None, :], T, nllr=nllr, hist=nllr)
+        self.convergence_iteration = int(r.conv[0])
+        p_data_buffer._decoded_data = r.z[0].astype(np.int64).tolist()
+        if nllr:
+            k = self.m_pData._n - self.m_pData._m
+            done = int(r.iters[0])
+            vals = r.hist[0, :done]
+            self._normalized_llr_by_iterations.extend(float(v) for v in vals)
+            self._arr_changed_by_iterations.extend(int(round(v * k)) for v in vals)
+            if self._normalized_llr_by_iterations:
+                self._d_summarize_normalized_llr = self._normalized_llr_by_iterations[-1]
+        return self._Result.OK if r.status[0] == 0 else self._Result.DATA_TRANSFER_NOT_OK
+
+    # ------------------------------------------------------------ a batch
+    def decode_batch(self, llr, max_iter=None, nllr=None, post=False, hist=False, msgs=False,
+                     max_frames=None):
+        """Decode [B, n] LLRs.  Returns dict(z, conv, status, iters, nllr, post, hist, msgs)."""
+        T = int(self.m_pSettings.get_max_iterations() if max_iter is None else max_iter)
+        nl = bool(self.m_pSettings.is_normalized_llr_calculate() if nllr is None else nllr)
+        llr = np.asarray(llr, dtype=np.float64)
+        B = llr.shape[0] if llr.ndim == 2 else 1
+        dev = self._dev
+        want = max_frames or B
+        if want > dev.capacity:
+            dev = self._dev = Decoder(self._graph, want)
+        return dev.decode(llr, T, nllr=nl, post=post, hist=hist, msgs=msgs)

@@ -1,0 +1,234 @@
+/*
+ * spa_oracle.c -- CPU restatement of the reference SPA decoder.
+ *
+ * TEST INFRASTRUCTURE ONLY.  Nothing in the product path (ldpc-simulator_amd/)
+ * links, loads or calls this file; only tests/, __graft_entry__.smoke() and
+ * bench.py's cpu_baseline leg use it, as the checker / CPU baseline.
+ *
+ * Pinned against the reference: the tests/golden fixtures were produced by running
+ * /root/reference/python_ldpc_app/spa_decoder.py itself (tests/golden/gen_golden.py);
+ * tests/test_oracle_golden.py checks this restatement against every vector.
+ *
+ * Restates python_ldpc_app/spa_decoder.py:SPA_Decoder.decode (lines 63-280):
+ *   M init          :85-90     M[e] = ch[col(e)]
+ *   check-node pass :114-168   t = tanh(M/2) with the +-17.5 clip (:138-146),
+ *                              P = sequential product in ascending column order
+ *                              (np.prod, :151-152), q = P/t if |t|>1e-10 else the
+ *                              sequential product of the others (:159-164),
+ *                              q clipped to +-CL (:167), E = 2*atanh(q) (:168)
+ *   posterior       :173-185   L[j] = ch[j] + ((0+E[r0,j])+E[r1,j])+... (rows ascending)
+ *   hard decision   :188       z = (L < 0)
+ *   syndrome        :191-204   H_std . (z^1) mod 2
+ *   normalized LLR  :210-228   count over i<k, |L|<=7, apriori*L<0
+ *   exits           :231-253   OK at zero syndrome, NOT_OK at it == T-1
+ *   M update        :260-268   M[e] = L[col(e)] - E[e]
+ *   apriori update  :273-274
+ * The graph is H_std in CSR with ascending column indices (the reference's
+ * check_to_var order, spa_decoder.py:44-61 / encoder_decoder_data.py:215).
+ *
+ * Build: oracle/Makefile  ->  oracle/liboracle_spa.so  (gcc -O2, no fast-math,
+ * -ffp-contract=off so every product/sum is a single IEEE-rounded op).
+ */
+#include <math.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+#define ORACLE_CL 0.99999999999999878 /* spa_decoder.py:141,167 */
+#define ORACLE_TINY 1e-10             /* spa_decoder.py:159 */
+
+/*
+ * Conditioning probe (tests only): when non-zero, every tanh() result is moved
+ * by this many ulps toward zero.  Decoding a frame twice, with 0 and 1, shows
+ * how far ONE ulp of tanh -- the size of the numpy-SVML vs glibc difference --
+ * moves that frame's outputs.  Saturated frames (|q| within a few ulps of the
+ * +-CL clip) are ill-conditioned: there the reference's own LLRs are rounding
+ * noise at the 1e-3 level, and tests grant exactly that measured slack.
+ */
+static int g_tanh_nudge = 0;
+void oracle_set_tanh_nudge(int ulps) { g_tanh_nudge = ulps; }
+
+static double nudge(double t) {
+    for (int i = 0; i < g_tanh_nudge; ++i) t = nextafter(t, 0.0);
+    return t;
+}
+
+typedef struct {
+    int m, n, nnz;
+    const int *row_ptr, *col_idx;
+    int *csc_ptr;  /* n+1 */
+    int *csc_edge; /* nnz: CSR edge ids of column j, rows ascending */
+} oracle_graph;
+
+static int build_csc(oracle_graph *g) {
+    g->csc_ptr = (int *)calloc((size_t)g->n + 1, sizeof(int));
+    g->csc_edge = (int *)malloc(sizeof(int) * (size_t)(g->nnz > 0 ? g->nnz : 1));
+    if (!g->csc_ptr || !g->csc_edge) return -1;
+    for (int e = 0; e < g->nnz; ++e) g->csc_ptr[g->col_idx[e] + 1]++;
+    for (int j = 0; j < g->n; ++j) g->csc_ptr[j + 1] += g->csc_ptr[j];
+    int *fill = (int *)malloc(sizeof(int) * (size_t)(g->n > 0 ? g->n : 1));
+    if (!fill) return -1;
+    memcpy(fill, g->csc_ptr, sizeof(int) * (size_t)g->n);
+    for (int r = 0; r < g->m; ++r) /* rows ascending -> each column's list ascending */
+        for (int e = g->row_ptr[r]; e < g->row_ptr[r + 1]; ++e) g->csc_edge[fill[g->col_idx[e]]++] = e;
+    free(fill);
+    return 0;
+}
+
+static void free_csc(oracle_graph *g) {
+    free(g->csc_ptr);
+    free(g->csc_edge);
+}
+
+/* One frame.  Returns 0 (Result.OK) or 1 (Result.DATA_TRANSFER_NOT_OK). */
+static int decode_one(const oracle_graph *g, const double *ch, int max_iter, int nllr_on,
+                      uint8_t *z_out, int *conv_out, double *L_out, double *E_out, double *nllr_out,
+                      int *iters_out, double *M, double *E, double *t, double *L, double *apri,
+                      uint8_t *z) {
+    const int m = g->m, n = g->n, k = n - m;
+    for (int r = 0; r < m; ++r)
+        for (int e = g->row_ptr[r]; e < g->row_ptr[r + 1]; ++e) M[e] = ch[g->col_idx[e]];
+    memset(E, 0, sizeof(double) * (size_t)g->nnz);
+    memcpy(apri, ch, sizeof(double) * (size_t)n);
+    double nllr = 0.0;
+    int status = 1, conv = -1, it = 0;
+    for (;; ++it) {
+        /* check-node pass */
+        for (int r = 0; r < m; ++r) {
+            const int b = g->row_ptr[r], deg = g->row_ptr[r + 1] - b;
+            if (deg == 0) continue;
+            for (int i = 0; i < deg; ++i) {
+                const double d = M[b + i] / 2.0;
+                t[i] = d > 17.5 ? ORACLE_CL : (d < -17.5 ? -ORACLE_CL : nudge(tanh(d)));
+            }
+            double P = t[0];
+            for (int i = 1; i < deg; ++i) P = P * t[i];
+            for (int i = 0; i < deg; ++i) {
+                double q;
+                if (fabs(t[i]) > ORACLE_TINY) {
+                    q = P / t[i];
+                } else { /* np.prod(np.delete(tanh_array, idx)) */
+                    int first = 1;
+                    q = 1.0;
+                    for (int j = 0; j < deg; ++j) {
+                        if (j == i) continue;
+                        q = first ? t[j] : q * t[j];
+                        first = 0;
+                    }
+                }
+                q = q < -ORACLE_CL ? -ORACLE_CL : q; /* np.clip = min(max(q, lo), hi) */
+                q = q > ORACLE_CL ? ORACLE_CL : q;
+                E[b + i] = 2.0 * atanh(q);
+            }
+        }
+        /* posterior + hard decision */
+        for (int j = 0; j < n; ++j) {
+            double s = 0.0;
+            for (int p = g->csc_ptr[j]; p < g->csc_ptr[j + 1]; ++p) s = s + E[g->csc_edge[p]];
+            L[j] = ch[j] + s;
+            z[j] = (uint8_t)(L[j] < 0.0);
+        }
+        /* syndrome on z^1 */
+        int fail = 0;
+        for (int r = 0; r < m && !fail; ++r) {
+            int par = 0;
+            for (int e = g->row_ptr[r]; e < g->row_ptr[r + 1]; ++e) par ^= (z[g->col_idx[e]] ^ 1);
+            fail = par;
+        }
+        if (nllr_on) {
+            int cnt = 0;
+            for (int i = 0; i < k; ++i) {
+                if (fabs(L[i]) > 7.0) continue;
+                if (apri[i] * L[i] < 0.0) cnt++;
+            }
+            nllr = k > 0 ? (double)cnt / (double)k : 0.0;
+        }
+        if (!fail) {
+            status = 0;
+            conv = it;
+            break;
+        }
+        if (it == max_iter - 1) {
+            status = 1;
+            break;
+        }
+        for (int r = 0; r < m; ++r)
+            for (int e = g->row_ptr[r]; e < g->row_ptr[r + 1]; ++e) M[e] = L[g->col_idx[e]] - E[e];
+        if (nllr_on) memcpy(apri, L, sizeof(double) * (size_t)n);
+    }
+    if (z_out) memcpy(z_out, z, (size_t)n);
+    if (conv_out) *conv_out = conv;
+    if (L_out) memcpy(L_out, L, sizeof(double) * (size_t)n);
+    if (E_out) memcpy(E_out, E, sizeof(double) * (size_t)g->nnz);
+    if (nllr_out) *nllr_out = nllr;
+    if (iters_out) *iters_out = it + 1;
+    return status;
+}
+
+/*
+ * Batch entry.  llr: [batch][n] in H_std column order.  Outputs are [batch][...]
+ * and each may be NULL.  threads<=0 -> OpenMP default.  Returns 0, or -1 on bad
+ * arguments / allocation failure (max_iter < 1 is rejected: the reference would
+ * loop until the syndrome clears, spa_decoder.py:104).
+ */
+int oracle_spa_decode_batch(int m, int n, const int *row_ptr, const int *col_idx, int batch,
+                            const double *llr, int max_iter, int nllr_on, int threads,
+                            uint8_t *z_out, int *conv_out, int *status_out, double *L_out,
+                            double *E_out, double *nllr_out, int *iters_out) {
+    if (m < 0 || n <= 0 || batch < 0 || max_iter < 1 || !row_ptr || !col_idx || (batch > 0 && !llr))
+        return -1;
+    oracle_graph g = {m, n, row_ptr[m], row_ptr, col_idx, NULL, NULL};
+    if (build_csc(&g)) return -1;
+    int maxdeg = 1;
+    for (int r = 0; r < m; ++r)
+        if (row_ptr[r + 1] - row_ptr[r] > maxdeg) maxdeg = row_ptr[r + 1] - row_ptr[r];
+    int err = 0;
+#ifdef _OPENMP
+    if (threads > 0) omp_set_num_threads(threads);
+#pragma omp parallel reduction(| : err)
+#endif
+    {
+        const size_t nnz = (size_t)(g.nnz > 0 ? g.nnz : 1);
+        double *M = (double *)malloc(sizeof(double) * nnz);
+        double *E = (double *)malloc(sizeof(double) * nnz);
+        double *t = (double *)malloc(sizeof(double) * (size_t)maxdeg);
+        double *L = (double *)malloc(sizeof(double) * (size_t)n);
+        double *ap = (double *)malloc(sizeof(double) * (size_t)n);
+        uint8_t *z = (uint8_t *)malloc((size_t)n);
+        if (!M || !E || !t || !L || !ap || !z) {
+            err = 1;
+        } else {
+#ifdef _OPENMP
+#pragma omp for schedule(dynamic, 1)
+#endif
+            for (int f = 0; f < batch; ++f) {
+                const size_t F = (size_t)f;
+                int st = decode_one(&g, llr + F * n, max_iter, nllr_on, z_out ? z_out + F * n : NULL,
+                                    conv_out ? conv_out + f : NULL, L_out ? L_out + F * n : NULL,
+                                    E_out ? E_out + F * (size_t)g.nnz : NULL,
+                                    nllr_out ? nllr_out + f : NULL, iters_out ? iters_out + f : NULL,
+                                    M, E, t, L, ap, z);
+                if (status_out) status_out[f] = st;
+            }
+        }
+        free(M);
+        free(E);
+        free(t);
+        free(L);
+        free(ap);
+        free(z);
+    }
+    free_csc(&g);
+    return err ? -1 : 0;
+}
+
+int oracle_max_threads(void) {
+#ifdef _OPENMP
+    return omp_get_max_threads();
+#else
+    return 1;
+#endif
+}

@@ -1,0 +1,275 @@
+#!/usr/bin/env python3
+"""Generate the golden decode vectors that pin the oracle and the HIP path.
+
+Runs ONLY in the build container, where the reference is importable from
+/root/reference/python_ldpc_app (no permission denial).  It
+drives the reference itself -- EncoderDecoderData, DataBuffer, Channel,
+SPA_Decoder.decode -- on seeded inputs and writes small .npz fixtures next to
+this script.  The reference source never leaves this container; only the
+input/output vectors below are committed.
+
+What is captured per frame (reference spa_decoder.py:63-280):
+  u      info bits drawn by DataBuffer (random.seed(seed), data_buffer.py:23)
+  ch     channel LLRs in H_std column order (channel.py:38-81; RandomState seeded)
+  z      decoder hard output _decoded_data (the complement of the bit estimate)
+  conv   convergence_iteration (-1 if not converged)
+  ok     decode() == Result.OK
+  L      final a-posteriori LLRs  (f_locals['arr_aposteriori_llrs'] on return)
+  E      final check->variable messages in H_std CSR edge order (f_locals['E'])
+         -- full for BCH, every 97th edge for the larger codes, plus sha256
+  nllr   _d_summarize_normalized_llr when the normalized-LLR metric is on
+
+Per code (codes/<name>.npz): the ALIST-derived H (utils.py:21-113) as CSR,
+H_std CSR (full for small codes), the column permutation and sha256
+fingerprints of both.
+
+Usage:  python tests/golden/gen_golden.py [--only NAME ...]
+"""
+import argparse
+import hashlib
+import multiprocessing as mp
+import os
+import random
+import sys
+import time
+
+import numpy as np
+
+REF_APP = "/root/reference/python_ldpc_app"
+REF_DB = "/root/reference/Channel_Codes_Database"
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+CODES = {
+    "BCH_7_4_1_strip": "BCH_7_4_1_strip.alist.txt",
+    "wimax_576_0.5": "Wimax LDPC Codes/wimax_576_0.5.alist.txt",
+    "wimax_2304_0.5": "Wimax LDPC Codes/wimax_2304_0.5.alist.txt",
+    "wimax_2304_0.75A": "Wimax LDPC Codes/wimax_2304_0.75A.alist.txt",
+    "wimax_2304_0.75B": "Wimax LDPC Codes/wimax_2304_0.75B.alist.txt",
+}
+# codes whose full H_std is small enough to commit
+FULL_HSTD = {"BCH_7_4_1_strip", "wimax_576_0.5"}
+E_STRIDE = 97
+
+_EDD = {}  # name -> EncoderDecoderData (filled in the parent, inherited by fork)
+
+
+def _ref_imports():
+    os.environ["PYTHONDONTWRITEBYTECODE"] = "1"
+    sys.dont_write_bytecode = True
+    if REF_APP not in sys.path:
+        sys.path.insert(0, REF_APP)
+
+
+def sha16(*arrays):
+    h = hashlib.sha256()
+    for a in arrays:
+        h.update(np.ascontiguousarray(a).astype("<i4").tobytes())
+    return h.hexdigest()
+
+
+def load_code(name):
+    _ref_imports()
+    from encoder_decoder_data import EncoderDecoderData
+    from utils import read_parity_check_matrix
+
+    path = os.path.join(REF_DB, CODES[name])
+    t0 = time.time()
+    H = read_parity_check_matrix(path).get_sparse_matrix().tocsr()
+    edd = EncoderDecoderData(path)
+    print(f"[{name}] EncoderDecoderData built in {time.time()-t0:.1f}s", flush=True)
+    _EDD[name] = edd
+    hs = edd._h_sparse_cached.tocsr()
+    hs_sorted = hs.copy()
+    hs_sorted.sort_indices()
+    # the decoder walks H_std in its stored CSR order: it must already be canonical
+    assert np.array_equal(hs.indices, hs_sorted.indices), "H_std CSR not sorted"
+    out = dict(
+        name=np.array(name),
+        m=np.int32(H.shape[0]), n=np.int32(H.shape[1]),
+        h_indptr=H.indptr.astype(np.int32), h_indices=H.indices.astype(np.int32),
+        h_data=H.data.astype(np.int32),
+        m_std=np.int32(edd._m), k=np.int32(edd._k),
+        perm=np.asarray(edd._permutation, dtype=np.int32),
+        hstd_nnz=np.int64(hs.nnz),
+        hstd_sha=np.array(sha16(hs.indptr, hs.indices)),
+        perm_sha=np.array(sha16(np.asarray(edd._permutation))),
+    )
+    if name in FULL_HSTD:
+        out["hstd_indptr"] = hs.indptr.astype(np.int32)
+        out["hstd_indices"] = hs.indices.astype(np.int32)
+    np.savez_compressed(os.path.join(HERE, "codes", f"{name}.npz"), **out)
+    return edd
+
+
+def _capture_decode(dec, db):
+    """Run dec.decode(db) and grab the final L and E from the frame locals."""
+    captured = {}
+    target = type(dec).decode.__code__
+
+    def local_tracer(frame, event, arg):
+        if event == "return":
+            captured["L"] = np.array(frame.f_locals["arr_aposteriori_llrs"], dtype=np.float64)
+            captured["E"] = frame.f_locals["E"].tocsr()
+        return local_tracer
+
+    def global_tracer(frame, event, arg):
+        if event == "call" and frame.f_code is target:
+            return local_tracer
+        return None
+
+    sys.settrace(global_tracer)
+    try:
+        res = dec.decode(db)
+    finally:
+        sys.settrace(None)
+    return res, captured
+
+
+def run_frame(job):
+    """One reference decode.  job = (code, T, snr, seed, nllr, ch_override)."""
+    _ref_imports()
+    from channel import Channel
+    from data_buffer import DataBuffer
+    from enums import LDPCDecoderType, Result
+    from settings import Settings
+    from spa_decoder import SPA_Decoder
+
+    name, T, snr, seed, nllr, ch_override = job
+    edd = _EDD[name]
+    settings = Settings()
+    settings.set_max_iterations(T)
+    settings.set_decoder_type(LDPCDecoderType.SUM_PRODUCT)
+    settings.set_normalized_llr_calculate(bool(nllr))
+
+    random.seed(seed)
+    db = DataBuffer(edd._k)
+    db.encode(edd._g_transpose)
+    chan = Channel.create_channel(1.0, snr, 0.0, 1, 0.1, 1)
+    chan._rng = np.random.RandomState((seed * 7919 + 12345) % (2**31))
+    chan.process(db)
+    if ch_override is not None:
+        db._channel_data = [float(x) for x in ch_override]
+
+    dec = SPA_Decoder(edd, settings)
+    res, cap = _capture_decode(dec, db)
+
+    hs = edd._h_sparse_cached.tocsr()
+    coo = hs.tocoo()
+    E = cap["E"]
+    e_vals = np.asarray(E[coo.row, coo.col]).ravel().astype(np.float64)
+    return dict(
+        u=np.asarray(db._data, dtype=np.uint8),
+        ch=np.asarray(db._channel_data, dtype=np.float64),
+        z=np.asarray(db._decoded_data, dtype=np.uint8),
+        conv=np.int32(dec.convergence_iteration),
+        ok=bool(res == Result.OK),
+        L=cap["L"],
+        E=e_vals,
+        nllr=np.float64(dec._d_summarize_normalized_llr),
+        nllr_iters=np.asarray(dec._normalized_llr_by_iterations, dtype=np.float64),
+    )
+
+
+def run_set(pool, set_name, code, T, snrs, frames, nllr, base_seed, overrides=None):
+    jobs = []
+    meta_snr = []
+    for si, snr in enumerate(snrs):
+        for f in range(frames):
+            seed = base_seed + si * 100003 + f
+            ov = None
+            if overrides is not None:
+                ov = overrides[len(jobs)]
+            jobs.append((code, T, snr, seed, nllr, ov))
+            meta_snr.append(snr)
+    t0 = time.time()
+    outs = pool.map(run_frame, jobs, chunksize=1)
+    full_e = code not in FULL_HSTD or code == "BCH_7_4_1_strip"
+    E_all = np.stack([o["E"] for o in outs])
+    rec = dict(
+        code=np.array(code), T=np.int32(T), nllr_on=np.bool_(nllr),
+        snr=np.asarray(meta_snr, dtype=np.float64),
+        seed=np.asarray([j[3] for j in jobs], dtype=np.int64),
+        u=np.stack([o["u"] for o in outs]),
+        ch=np.stack([o["ch"] for o in outs]),
+        z=np.stack([o["z"] for o in outs]),
+        conv=np.asarray([o["conv"] for o in outs], dtype=np.int32),
+        ok=np.asarray([o["ok"] for o in outs], dtype=np.bool_),
+        L=np.stack([o["L"] for o in outs]),
+        nllr=np.asarray([o["nllr"] for o in outs], dtype=np.float64),
+        e_sha=np.array([hashlib.sha256(e.astype("<f8").tobytes()).hexdigest() for e in E_all]),
+        e_stride=np.int32(1 if code == "BCH_7_4_1_strip" else E_STRIDE),
+    )
+    rec["E"] = E_all if code == "BCH_7_4_1_strip" else E_all[:, ::E_STRIDE].copy()
+    del full_e
+    np.savez_compressed(os.path.join(HERE, f"{set_name}.npz"), **rec)
+    print(f"[{set_name}] {len(jobs)} frames in {time.time()-t0:.1f}s; "
+          f"ok={rec['ok'].mean():.3f} conv>=0:{(rec['conv']>=0).sum()}", flush=True)
+
+
+def edge_overrides(n, frames, rng, kind):
+    """Channel LLR vectors that force the rare branches of spa_decoder.py."""
+    out = []
+    for f in range(frames):
+        if kind == "zeros":
+            # exact zeros -> tanh(0)=0 -> |t|<=1e-10 branch (spa_decoder.py:159-164)
+            ch = rng.normal(0.0, 2.0, n)
+            idx = rng.choice(n, size=max(1, n // 50), replace=False)
+            ch[idx] = 0.0
+            if f % 2 == 1:
+                ch[rng.choice(n, size=max(1, n // 100), replace=False)] = 1e-12
+        elif kind == "saturate":
+            # |M/2|>17.5 clip (spa_decoder.py:140-143) and atanh clip (:167)
+            ch = rng.choice([-1.0, 1.0], n) * rng.uniform(30.0, 80.0, n)
+            ch[rng.choice(n, size=max(1, n // 10), replace=False)] *= -0.05
+        else:
+            raise ValueError(kind)
+        out.append(ch)
+    return out
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--only", nargs="*", default=None)
+    ap.add_argument("--procs", type=int, default=8)
+    args = ap.parse_args()
+    want = lambda s: args.only is None or s in args.only  # noqa: E731
+
+    os.makedirs(os.path.join(HERE, "codes"), exist_ok=True)
+    need = set()
+    if want("codes") or want("bch"):
+        need.add("BCH_7_4_1_strip")
+    if want("codes") or any(want(s) for s in ("w576_T5", "w576_T50", "w576_edge")):
+        need.add("wimax_576_0.5")
+    if want("codes") or want("w2304_T3"):
+        need.add("wimax_2304_0.5")
+    if want("codes") or want("w2304A_T2"):
+        need.add("wimax_2304_0.75A")
+    if want("codes"):
+        need.add("wimax_2304_0.75B")
+    for name in CODES:
+        if name in need:
+            load_code(name)
+
+    ctx = mp.get_context("fork")
+    rng = np.random.default_rng(20260213)
+    with ctx.Pool(args.procs) as pool:
+        if want("bch"):
+            run_set(pool, "bch_T10", "BCH_7_4_1_strip", 10, [0.0, 2.0, 4.0, 6.0], 250, True, 1000)
+            ov = edge_overrides(7, 16, rng, "zeros") + edge_overrides(7, 16, rng, "saturate")
+            run_set(pool, "bch_edge_T1", "BCH_7_4_1_strip", 1, [4.0], 32, True, 5000, ov)
+            run_set(pool, "bch_edge_T3", "BCH_7_4_1_strip", 3, [4.0], 32, True, 6000, ov)
+        if want("w576_T5"):
+            run_set(pool, "w576_T5", "wimax_576_0.5", 5, [0.0, 1.0, 2.0, 3.0], 16, True, 2000)
+        if want("w576_T50"):
+            run_set(pool, "w576_T50", "wimax_576_0.5", 50, [0.0, 2.0], 8, False, 3000)
+        if want("w576_edge"):
+            ov = edge_overrides(576, 4, rng, "zeros") + edge_overrides(576, 4, rng, "saturate")
+            run_set(pool, "w576_edge", "wimax_576_0.5", 5, [2.0], 8, True, 4000, ov)
+        if want("w2304_T3"):
+            run_set(pool, "w2304_T3", "wimax_2304_0.5", 3, [0.0, 3.0], 2, True, 7000)
+        if want("w2304A_T2"):
+            run_set(pool, "w2304A_T2", "wimax_2304_0.75A", 2, [2.0], 2, False, 8000)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,130 @@
+"""GPU parity: the HIP decoder (through the C ABI) vs the reference and the oracle.
+
+1. Golden vectors (made by the reference itself): hard bits, convergence
+   iteration and Result bit-exact; posterior L and messages E within 1e-5
+   relative; normalized LLR exact.
+2. Seeded random batches vs the pinned CPU oracle at sizes it finishes in
+   seconds: same bar.
+3. Edge cases the reference has: max_iter=1, exact-zero LLRs (|t|<=1e-10
+   branch), saturating LLRs (both clips), ragged batches (not a multiple of the
+   64-frame tile), chunking (batch larger than the decoder's capacity), an
+   empty batch, and max_iter<1 rejected.
+"""
+import numpy as np
+import pytest
+
+import oracle
+from conftest import GOLDEN_SETS, assert_llr_close, hstd_for, load_golden
+
+pytestmark = pytest.mark.gpu
+
+
+def _decoder(code, frames):
+    from ldpc_amd.device import Decoder, Graph
+    return Decoder(Graph.cached(hstd_for(code)), frames)
+
+
+@pytest.mark.parametrize("set_name", GOLDEN_SETS)
+def test_gpu_matches_reference_golden(gpu_available, set_name):
+    g = load_golden(set_name)
+    code = str(g["code"])
+    nl = bool(g["nllr_on"])
+    dec = _decoder(code, len(g["ch"]))
+    r = dec.decode(g["ch"], int(g["T"]), nllr=nl, post=True, hist=nl, msgs=True)
+    sl_L, sl_E = oracle.conditioning_slack(hstd_for(code), g["ch"], int(g["T"]), nllr=nl)
+    np.testing.assert_array_equal(r.z, g["z"], err_msg="hard decisions")
+    np.testing.assert_array_equal(r.conv, g["conv"], err_msg="convergence_iteration")
+    np.testing.assert_array_equal(r.status == 0, g["ok"], err_msg="Result")
+    assert_llr_close(r.post, g["L"], "posterior L", slack=sl_L)
+    assert_llr_close(r.msgs[:, :: int(g["e_stride"])], g["E"], "messages E",
+                     slack=sl_E[:, :: int(g["e_stride"])])
+    if nl:
+        np.testing.assert_array_equal(r.nllr, g["nllr"], err_msg="normalized LLR")
+    iters = np.where(g["conv"] >= 0, g["conv"] + 1, int(g["T"]))
+    np.testing.assert_array_equal(r.iters, iters)
+
+
+def _random_llr(H, B, snr_db, seed):
+    """Channel LLRs of random codewords (reference channel model, numpy RNG)."""
+    rng = np.random.default_rng(seed)
+    m, n = H.shape
+    k = n - m
+    u = rng.integers(0, 2, size=(B, k))
+    par = (H[:, :k] @ u.T).T % 2
+    c = np.concatenate([u, par], axis=1)
+    sigma = oracle.sigma_for_snr(snr_db)
+    y = (2.0 * c - 1.0) + sigma ** 2 * rng.standard_normal((B, n))
+    return (2.0 * y) / sigma ** 2
+
+
+@pytest.mark.parametrize("code,B,T,snr", [
+    ("BCH_7_4_1_strip", 4096, 10, 1.0),
+    ("wimax_576_0.5", 200, 8, 1.5),
+    ("wimax_576_0.5", 130, 20, 2.5),
+    ("wimax_2304_0.75A", 64, 3, 3.0),
+])
+def test_gpu_matches_oracle_random(gpu_available, code, B, T, snr):
+    H = hstd_for(code)
+    llr = _random_llr(H, B, snr, seed=B * 31 + T)
+    dec = _decoder(code, B)
+    r = dec.decode(llr, T, nllr=True, post=True)
+    o = oracle.spa_decode(H, llr, T, nllr=True)
+    np.testing.assert_array_equal(r.z, o["z"])
+    np.testing.assert_array_equal(r.conv, o["conv"])
+    np.testing.assert_array_equal(r.status, o["status"])
+    np.testing.assert_array_equal(r.iters, o["iters"])
+    np.testing.assert_array_equal(r.nllr, o["nllr"])
+    assert_llr_close(r.post, o["post"], "posterior L")
+
+
+def test_gpu_edge_cases(gpu_available):
+    code = "wimax_576_0.5"
+    H = hstd_for(code)
+    rng = np.random.default_rng(7)
+    llr = _random_llr(H, 70, 2.0, seed=3)             # ragged: 70 = 64 + 6
+    llr[0, :] = 0.0                                    # all-zero frame: every t == 0
+    llr[1, ::7] = 0.0                                  # sparse exact zeros
+    llr[2, :] = rng.choice([-1, 1], 576) * 60.0        # saturating
+    llr[3, :] = 1e-13                                  # tiny everywhere
+    llr[4, :] = -np.abs(llr[4, :])                     # all-ones-ish hard decision
+    for T in (1, 2, 5):
+        dec = _decoder(code, 70)
+        r = dec.decode(llr, T, nllr=True, post=True, msgs=True)
+        o = oracle.spa_decode(H, llr, T, nllr=True, want_E=True)
+        sl_L, sl_E = oracle.conditioning_slack(H, llr, T)
+        np.testing.assert_array_equal(r.z, o["z"])
+        np.testing.assert_array_equal(r.conv, o["conv"])
+        np.testing.assert_array_equal(r.status, o["status"])
+        assert_llr_close(r.post, o["post"], f"L T={T}", slack=sl_L)
+        assert_llr_close(r.msgs, o["msgs"], f"E T={T}", slack=sl_E)
+
+
+def test_gpu_chunking_matches_single_chunk(gpu_available):
+    """A batch larger than the workspace runs in chunks with identical results."""
+    code = "wimax_576_0.5"
+    H = hstd_for(code)
+    llr = _random_llr(H, 300, 2.0, seed=11)
+    big = _decoder(code, 300).decode(llr, 6, post=True)
+    small = _decoder(code, 64).decode(llr, 6, post=True)
+    for key in ("z", "conv", "status", "iters"):
+        np.testing.assert_array_equal(big[key], small[key])
+    np.testing.assert_array_equal(big.post, small.post)
+
+
+def test_gpu_empty_batch_and_bad_iterations(gpu_available):
+    from ldpc_amd import LdpcError
+    dec = _decoder("BCH_7_4_1_strip", 64)
+    r = dec.decode(np.zeros((0, 7)), 5)
+    assert r.z.shape == (0, 7)
+    with pytest.raises(LdpcError):
+        dec.decode(np.zeros((1, 7)), 0)
+
+
+def test_gpu_deterministic(gpu_available):
+    code = "wimax_576_0.5"
+    llr = _random_llr(hstd_for(code), 128, 1.0, seed=5)
+    dec = _decoder(code, 128)
+    a = dec.decode(llr, 10, post=True, msgs=True)
+    b = dec.decode(llr, 10, post=True, msgs=True)
+    np.testing.assert_array_equal(a.post, b.post)
+    np.testing.assert_array_equal(a.msgs, b.msgs)
