@@ -50,7 +50,7 @@ struct ldpc_graph {
 struct ldpc_decoder {
     const ldpc_graph *g = nullptr;
     int cap_tiles = 0;
-    double *E = nullptr, *L = nullptr, *ch = nullptr;
+    double *E = nullptr, *T = nullptr, *L = nullptr, *ch = nullptr;
     int *ints = nullptr;  // done, conv, status, iters, nllr_cnt (cap frames each) + tile_active
     uint32_t *ubits = nullptr;
     // staging for host I/O
@@ -105,6 +105,7 @@ void state_bind(ldpc_decoder *d, int ntiles, int count) {
     const size_t cap = (size_t)d->cap_tiles * kTile;
     DevState &s = d->st;
     s.E = d->E;
+    s.T = d->T;
     s.L = d->L;
     s.ch = d->ch;
     s.done = d->ints;
@@ -158,7 +159,7 @@ size_t workspace_bytes(const DevGraph &g, int cap_tiles) {
     const size_t cap = (size_t)cap_tiles * kTile;
     const size_t kw = (size_t)((g.k + 31) / 32);
     size_t b = 0;
-    b += cap * (size_t)g.nnz * 8;      // E
+    b += 2 * cap * (size_t)g.nnz * 8;  // E, T
     b += 2 * cap * (size_t)g.n * 8;    // L, ch
     b += (5 * cap + cap_tiles) * 4;    // per-frame ints + tile flags
     b += cap * kw * 4;                 // ubits
@@ -314,6 +315,7 @@ int ldpc_decoder_create(const ldpc_graph *g, int32_t max_frames, ldpc_decoder **
     const size_t kw = (size_t)((G.k + 31) / 32);
     int rc = LDPC_OK;
     if (!rc) rc = dev_alloc(&d->E, cap * (size_t)G.nnz);
+    if (!rc) rc = dev_alloc(&d->T, cap * (size_t)G.nnz);
     if (!rc) rc = dev_alloc(&d->L, cap * (size_t)G.n);
     if (!rc) rc = dev_alloc(&d->ch, cap * (size_t)G.n);
     if (!rc) rc = dev_alloc(&d->ints, 5 * cap + (size_t)d->cap_tiles);
@@ -333,6 +335,7 @@ int ldpc_decoder_destroy(ldpc_decoder *d) {
     if (!d) return LDPC_OK;
     DeviceGuard dg(d->g ? d->g->device : -1);
     (void)hipFree(d->E);
+    (void)hipFree(d->T);
     (void)hipFree(d->L);
     (void)hipFree(d->ch);
     (void)hipFree(d->ints);

@@ -6,6 +6,7 @@
 // 64 consecutive doubles (512 contiguous bytes): fully coalesced, with no
 // index math per lane.
 //   E   [tile][nnz][64]  fp64 check->variable messages (CSR edge order of H_std)
+//   T   [tile][nnz][64]  fp64 scratch: tanh(M/2) parked between the CN passes
 //   L   [tile][n][64]    fp64 a-posteriori LLRs
 //   ch  [tile][n][64]    fp64 channel LLRs
 //   ub  [tile][kw][64]   info bits (Monte-Carlo path), kw = ceil(k/32)
@@ -30,7 +31,7 @@ struct DevGraph {
 };
 
 struct DevState {
-    double *E, *L, *ch;
+    double *E, *T, *L, *ch;
     int *done, *conv, *status, *iters, *nllr_cnt;
     int *tile_active;
     uint32_t *ubits;         // MC only (may be null)

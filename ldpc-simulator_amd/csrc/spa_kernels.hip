@@ -12,8 +12,9 @@
 //                P = t0*t1*...  strictly left to right          (np.prod, :152)
 //                q = P/t (|t|>1e-10) else prod of the others    (:159-164)
 //                E = 2*atanh(clip(q, +-CL))                     (:167-168)
-//              t is parked in E's slot between the two passes (same lane, same
-//              address), so the kernel needs no scratch.
+//              t is parked in a scratch array T (same [tile][edge][64] layout)
+//              between the two passes: pass 2 overwrites E in place while the
+//              rare "product of the others" branch still re-reads every t.
 //   vn_kernel  one workgroup (16 wavefronts) per tile; wavefront w takes
 //              columns w, w+16, ...:
 //                L = ch + ((0+E[r0])+E[r1])+...  rows ascending (:173-185)
@@ -76,6 +77,7 @@ __global__ __launch_bounds__(256) void cn_kernel(DevGraph g, DevState st, int bl
     const int f = tile * kTile + lane;
     const bool live = st.done[f] == 0;
     double *Et = st.E + (size_t)tile * g.nnz * kTile + lane;
+    double *Tt = st.T + (size_t)tile * g.nnz * kTile + lane;
     const double *Lt = (kFirst ? st.ch : st.L) + (size_t)tile * g.n * kTile + lane;
 
     double P = 1.0;
@@ -85,10 +87,10 @@ __global__ __launch_bounds__(256) void cn_kernel(DevGraph g, DevState st, int bl
         if (!kFirst) M = M - Et[e * kTile];
         const double t = cn_tanh(M);
         P = (e == beg) ? t : P * t;
-        if (live) Et[e * kTile] = t;
+        Tt[e * kTile] = t;
     }
     for (int e = beg; e < end; ++e) {
-        const double t = Et[e * kTile];
+        const double t = Tt[e * kTile];
         double q;
         if (fabs(t) > kTiny) {
             q = P / t;
@@ -97,7 +99,7 @@ __global__ __launch_bounds__(256) void cn_kernel(DevGraph g, DevState st, int bl
             bool first = true;
             for (int e2 = beg; e2 < end; ++e2) {
                 if (e2 == e) continue;
-                const double t2 = Et[e2 * kTile];
+                const double t2 = Tt[e2 * kTile];
                 q = first ? t2 : q * t2;
                 first = false;
             }
