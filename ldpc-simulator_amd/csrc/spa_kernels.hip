@@ -28,14 +28,16 @@
 //
 // Numerics: fp64 throughout; this file is compiled with -ffp-contract=off and
 // without fast-math, so every +,-,*,/ is one correctly rounded IEEE op in the
-// reference's order.  tanh/atanh come from the ROCm device library (<=1-2 ulp,
-// as numpy's own SVML/glibc versions are).
+// reference's order.  tanh is numpy's own float64 algorithm (bit-identical
+// to the reference's np.tanh); atanh is correctly rounded on > 99% of inputs
+// (spa_math.h).  Their coefficient tables are staged in LDS per block.
 #include <hip/hip_runtime.h>
 
 #include <cmath>
 #include <cstdint>
 
 #include "spa_device.h"
+#include "spa_math.h"
 
 namespace ldpc {
 namespace {
@@ -52,14 +54,49 @@ __device__ __forceinline__ double clip_cl(double q) {
     return q > kCL ? kCL : q;
 }
 
-__device__ __forceinline__ double cn_tanh(double M) {
+// ---- math tables in LDS (9 x 16 tanh pairs + 128 log entries = 6.4 KB)
+struct LdsTanh {
+    const Pair *p;
+    __device__ __forceinline__ Pair operator()(int pp, int i) const { return p[pp * 16 + i]; }
+};
+struct alignas(16) LogEntry4 {
+    double invc, hi, lo, pad;
+};
+struct LdsLog {
+    const LogEntry4 *e;
+    __device__ __forceinline__ LogEntry operator()(int i) const {
+        const LogEntry4 v = e[i];
+        return {v.invc, v.hi, v.lo};
+    }
+};
+struct MathLds {
+    Pair tanh[9 * 16];
+    LogEntry4 log[128];
+};
+
+__device__ __forceinline__ void fill_math_lds(MathLds &m) {
+    for (int k = threadIdx.x; k < 9 * 16; k += blockDim.x) {
+        const int pp = k >> 4, i = k & 15;
+        m.tanh[k] = pp == 0 ? Pair{dfrom(tab::kTanhB[i]), dfrom(tab::kTanhC[0][i])}
+                            : Pair{dfrom(tab::kTanhC[2 * pp - 1][i]), dfrom(tab::kTanhC[2 * pp][i])};
+    }
+    for (int i = threadIdx.x; i < 128; i += blockDim.x)
+        m.log[i] = {dfrom(tab::kLog[i][0]), dfrom(tab::kLog[i][1]), dfrom(tab::kLog[i][2]), 0.0};
+}
+
+__device__ __forceinline__ double cn_tanh(double M, const LdsTanh &t) {
     const double d = M * 0.5;  // == M/2.0 bit for bit (power-of-two scale)
-    return d > 17.5 ? kCL : (d < -17.5 ? -kCL : tanh(d));
+    return d > 17.5 ? kCL : (d < -17.5 ? -kCL : np_tanh(d, t));
 }
 
 // --------------------------------------------------------------- CN pass
 template <bool kFirst>
 __global__ __launch_bounds__(256) void cn_kernel(DevGraph g, DevState st, int blocks_per_tile) {
+    __shared__ MathLds mlds;
+    fill_math_lds(mlds);
+    __syncthreads();
+    const LdsTanh ttab{mlds.tanh};
+    const LdsLog ltab{mlds.log};
     const int lane = threadIdx.x & 63;
     const int wave = uniform(threadIdx.x >> 6);
     // XCD-aware mapping: blocks b and b+8 share an XCD (round-robin dispatch),
@@ -85,7 +122,7 @@ __global__ __launch_bounds__(256) void cn_kernel(DevGraph g, DevState st, int bl
         const int c = g.col_idx[e];
         double M = Lt[c * kTile];
         if (!kFirst) M = M - Et[e * kTile];
-        const double t = cn_tanh(M);
+        const double t = cn_tanh(M, ttab);
         P = (e == beg) ? t : P * t;
         Tt[e * kTile] = t;
     }
@@ -104,7 +141,7 @@ __global__ __launch_bounds__(256) void cn_kernel(DevGraph g, DevState st, int bl
                 first = false;
             }
         }
-        const double En = 2.0 * atanh(clip_cl(q));
+        const double En = 2.0 * atanh_f(clip_cl(q), ltab);
         if (live) Et[e * kTile] = En;
     }
 }

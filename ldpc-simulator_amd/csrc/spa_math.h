@@ -1,0 +1,143 @@
+// spa_math.h -- fp64 tanh / atanh of the check-node update, host+device.
+//
+// np_tanh  numpy 2.2.6's float64 tanh (the reference's np.tanh,
+//          spa_decoder.py:145): 16 intervals selected from the exponent and
+//          top mantissa bit of |x|, y = |x| - b[i], degree-16 Horner with
+//          fused multiply-adds (c16 .. c0), |x| >= 24 -> 1, sign OR-ed back.
+//          Bit-identical to np.tanh (tests/test_math.py), so the parked
+//          t = tanh(M/2) values -- and with them P, q = P/t and the clip
+//          decisions -- are the reference's own bits.  On the GPU the
+//          coefficients sit in LDS as {b,c0},{c1,c2},...,{c15,c16} pairs:
+//          9 ds_read_b128 + 16 v_fma_f64 per call.
+// atanh_f  atanh for |q| <= CL (spa_decoder.py:167-168), our design:
+//          |q| < 2^-5: odd Taylor polynomial; else
+//          atanh(a) = (log1p(a) - log1p(-a)) / 2 with each log1p = log(1 +- a)
+//          plus its exact rounding correction, log from a 128-entry
+//          {1/c, -log(1/c)} table and a degree-8 polynomial (glibc-style
+//          reduction r = z/c - 1 by one fma).  About 0.51 ulp; it agrees with
+//          numpy's own arctanh on > 99% of inputs and is faithful on all.
+//          (numpy's arctanh is Intel SVML, which relies on x86-only
+//          reciprocal approximations and cannot be restated portably.)
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "spa_math_tables.h"
+
+namespace ldpc {
+
+__host__ __device__ __forceinline__ uint64_t dbits(double x) { return __builtin_bit_cast(uint64_t, x); }
+__host__ __device__ __forceinline__ double dfrom(uint64_t u) { return __builtin_bit_cast(double, u); }
+
+struct alignas(16) Pair {
+    double a, b;
+};
+
+// ----------------------------------------------------------------- tanh
+// tab(p, i) returns {b, c0} for p = 0 and {c(2p-1), c(2p)} for p = 1..8.
+template <class Tab>
+__host__ __device__ __forceinline__ double np_tanh(double x, const Tab &tab) {
+    const uint64_t ux = dbits(x);
+    const uint64_t nd = ux & 0x7ff8000000000000ull;
+    int hi = (int)(nd >> 32) - 0x3fc00000;
+    hi = hi < 0 ? 0 : (hi > 0x780000 ? 0x780000 : hi);
+    const int i = hi >> 19;
+    const Pair p0 = tab(0, i);
+    const double y = __builtin_fabs(x) - p0.a;
+    Pair c = tab(8, i);
+    double r = __builtin_fma(c.b, y, c.a);  // c16*y + c15
+#pragma unroll
+    for (int p = 7; p >= 1; --p) {
+        c = tab(p, i);
+        r = __builtin_fma(r, y, c.b);
+        r = __builtin_fma(r, y, c.a);
+    }
+    r = __builtin_fma(r, y, p0.b);
+    if (nd > 0x7fe0000000000000ull) r = 1.0;  // huge, inf (NaN -> 1 too; never reached here)
+    return dfrom(dbits(r) | (ux & 0x8000000000000000ull));
+}
+
+// ----------------------------------------------------------------- log
+constexpr double kLn2Hi = 0x1.62e42fefa3800p-1;  // 11 trailing zero bits: k*kLn2Hi exact
+constexpr double kLn2Lo = 0x1.ef35793c76730p-45;
+
+struct LogEntry {
+    double invc, hi, lo;
+};
+
+// log(x) = hi + lo for a positive normal x.  Accurate away from x ~ 1 (the
+// interval holding 1.0 itself is exact: invc = 1), which is all atanh needs.
+template <class LogTab>
+__host__ __device__ __forceinline__ void log_hilo(double x, const LogTab &lt, double &hi, double &lo) {
+    const uint64_t ix = dbits(x);
+    const uint64_t tmp = ix - 0x3fe6000000000000ull;
+    const int i = (int)((tmp >> 45) & 127);
+    const int k = (int)((int64_t)tmp >> 52);
+    const double z = dfrom(ix - (tmp & (0xfffull << 52)));
+    const LogEntry t = lt(i);
+    const double r = __builtin_fma(z, t.invc, -1.0);  // |r| < 2^-7
+    const double kd = (double)k;
+    const double w = __builtin_fma(kd, kLn2Hi, t.hi);  // exact
+    hi = w + r;
+    const double r2 = r * r;
+    // log1p(r) - r, Taylor to r^8
+    double p = __builtin_fma(r, -0.125, 0x1.2492492492492p-3);   // -1/8, 1/7
+    p = __builtin_fma(p, r, -0x1.5555555555555p-3);               // -1/6
+    p = __builtin_fma(p, r, 0x1.999999999999ap-3);                // 1/5
+    p = __builtin_fma(p, r, -0.25);                               // -1/4
+    p = __builtin_fma(p, r, 0x1.5555555555555p-2);                // 1/3
+    p = __builtin_fma(p, r, -0.5);                                // -1/2
+    lo = ((w - hi) + r) + (__builtin_fma(kd, kLn2Lo, t.lo) + r2 * p);
+}
+
+__host__ __device__ __forceinline__ double fast_div(double n, double d) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return n * __builtin_amdgcn_rcp(d);  // n is a rounding error: 1-ulp rcp is plenty
+#else
+    return n / d;
+#endif
+}
+
+// atanh(q) for |q| <= CL.
+template <class LogTab>
+__host__ __device__ __forceinline__ double atanh_f(double q, const LogTab &lt) {
+    const double a = __builtin_fabs(q);
+    double res;
+    if (a < 0x1p-5) {
+        const double a2 = a * a;
+        double p = __builtin_fma(a2, 1.0 / 13.0, 1.0 / 11.0);
+        p = __builtin_fma(p, a2, 1.0 / 9.0);
+        p = __builtin_fma(p, a2, 1.0 / 7.0);
+        p = __builtin_fma(p, a2, 0.2);
+        p = __builtin_fma(p, a2, 1.0 / 3.0);
+        res = __builtin_fma(a * a2, p, a);
+    } else {
+        const double u = 1.0 + a, v = 1.0 - a;
+        const double cu = fast_div(a - (u - 1.0), u);   // exact numerators (u-1, v-1 exact)
+        const double cv = fast_div(-a - (v - 1.0), v);  // 0 for a >= 0.5 (1-a exact)
+        double h1, l1, h2, l2;
+        log_hilo(u, lt, h1, l1);
+        log_hilo(v, lt, h2, l2);
+        const double s = h1 - h2;  // h1 > 0 > h2: no cancellation
+        const double bb = s - h1;
+        const double e = (h1 - (s - bb)) + (-h2 - bb);
+        res = 0.5 * (s + (e + ((l1 - l2) + (cu - cv))));
+    }
+    return dfrom(dbits(res) | (dbits(q) & 0x8000000000000000ull));
+}
+
+// Host-side table views (tests, host build of this header).
+struct HostTanhTab {
+    __host__ Pair operator()(int p, int i) const {
+        if (p == 0) return {dfrom(tab::kTanhB[i]), dfrom(tab::kTanhC[0][i])};
+        return {dfrom(tab::kTanhC[2 * p - 1][i]), dfrom(tab::kTanhC[2 * p][i])};
+    }
+};
+struct HostLogTab {
+    __host__ LogEntry operator()(int i) const {
+        return {dfrom(tab::kLog[i][0]), dfrom(tab::kLog[i][1]), dfrom(tab::kLog[i][2])};
+    }
+};
+
+}  // namespace ldpc

@@ -41,6 +41,8 @@ def lib():
         L.oracle_philox4x32_10.restype = None
         L.oracle_philox4x32_10.argtypes = [vp, ctypes.c_uint32, ctypes.c_uint32]
         L.oracle_max_threads.restype = ctypes.c_int
+        L.oracle_np_tanh.restype = dbl
+        L.oracle_np_tanh.argtypes = [dbl]
         L.oracle_set_tanh_nudge.restype = None
         L.oracle_set_tanh_nudge.argtypes = [i32]
         _lib = L
@@ -92,6 +94,12 @@ def conditioning_slack(H_std, llr, max_iter, nllr=False, factor=4.0):
     finally:
         lib().oracle_set_tanh_nudge(0)
     return factor * np.abs(pert["post"] - base["post"]), factor * np.abs(pert["msgs"] - base["msgs"])
+
+
+def np_tanh(x):
+    """The oracle's restatement of numpy's float64 tanh (elementwise)."""
+    f = lib().oracle_np_tanh
+    return np.array([f(float(v)) for v in np.asarray(x, dtype=np.float64).ravel()]).reshape(np.shape(x))
 
 
 def generate_frames(H_std, seed, snr_point, sigma, frame0, count):

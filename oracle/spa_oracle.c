@@ -37,7 +37,46 @@
 #include <omp.h>
 #endif
 
+#include "numpy_tanh_table.h"
+
 #define ORACLE_CL 0.99999999999999878 /* spa_decoder.py:141,167 */
+
+/*
+ * np.tanh, restated.  The reference calls numpy's float64 tanh
+ * (spa_decoder.py:145; numpy 2.2.6, an unpinned third-party dependency,
+ * requirements.txt:1).  numpy's published algorithm (loops_hyperbolic,
+ * SIMD dispatch AVX512_SKX): 16 intervals from the exponent and top mantissa
+ * bit of |x|, y = |x| - b[i], degree-16 Horner in fused multiply-adds, |x| >= 24
+ * (and huge / inf) -> 1, sign of x OR-ed back.  Bit-identical to np.tanh
+ * (tests/test_math.py).
+ */
+static double dfrom(unsigned long long u) {
+    double d;
+    memcpy(&d, &u, 8);
+    return d;
+}
+double oracle_np_tanh(double x) {
+    unsigned long long ux;
+    memcpy(&ux, &x, 8);
+    const unsigned long long nd = ux & 0x7ff8000000000000ULL;
+    int hi = (int)(nd >> 32) - 0x3fc00000;
+    hi = hi < 0 ? 0 : (hi > 0x780000 ? 0x780000 : hi);
+    const int i = hi >> 19;
+    const double y = fabs(x) - dfrom(NP_TANH_B[i]);
+    double r = fma(dfrom(NP_TANH_C[16][i]), y, dfrom(NP_TANH_C[15][i]));
+    for (int p = 14; p >= 0; --p) r = fma(r, y, dfrom(NP_TANH_C[p][i]));
+    if (nd > 0x7fe0000000000000ULL) r = 1.0;
+    unsigned long long ur;
+    memcpy(&ur, &r, 8);
+    ur |= ux & 0x8000000000000000ULL;
+    memcpy(&r, &ur, 8);
+    return r;
+}
+
+/* np.arctanh is Intel SVML (x86 reciprocal approximations, not restatable);
+ * it is correctly rounded on > 99.9% of inputs, and so is atanhl rounded to
+ * double -- the closest portable restatement. */
+static double oracle_atanh(double q) { return (double)atanhl((long double)q); }
 #define ORACLE_TINY 1e-10             /* spa_decoder.py:159 */
 
 /*
@@ -102,7 +141,7 @@ static int decode_one(const oracle_graph *g, const double *ch, int max_iter, int
             if (deg == 0) continue;
             for (int i = 0; i < deg; ++i) {
                 const double d = M[b + i] / 2.0;
-                t[i] = d > 17.5 ? ORACLE_CL : (d < -17.5 ? -ORACLE_CL : nudge(tanh(d)));
+                t[i] = d > 17.5 ? ORACLE_CL : (d < -17.5 ? -ORACLE_CL : nudge(oracle_np_tanh(d)));
             }
             double P = t[0];
             for (int i = 1; i < deg; ++i) P = P * t[i];
@@ -121,7 +160,7 @@ static int decode_one(const oracle_graph *g, const double *ch, int max_iter, int
                 }
                 q = q < -ORACLE_CL ? -ORACLE_CL : q; /* np.clip = min(max(q, lo), hi) */
                 q = q > ORACLE_CL ? ORACLE_CL : q;
-                E[b + i] = 2.0 * atanh(q);
+                E[b + i] = 2.0 * oracle_atanh(q);
             }
         }
         /* posterior + hard decision */
