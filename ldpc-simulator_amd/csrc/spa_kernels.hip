@@ -12,9 +12,11 @@
 //                P = t0*t1*...  strictly left to right          (np.prod, :152)
 //                q = P/t (|t|>1e-10) else prod of the others    (:159-164)
 //                E = 2*atanh(clip(q, +-CL))                     (:167-168)
-//              t is parked in a scratch array T (same [tile][edge][64] layout)
-//              between the two passes: pass 2 overwrites E in place while the
-//              rare "product of the others" branch still re-reads every t.
+//              Pass 1 only forms P; pass 2 recomputes t from the same E_old
+//              and L bits (24 B of HBM traffic per edge, not 32 B for parking
+//              t).  A wavefront holding some |t| <= 1e-10 instead parks t in a
+//              scratch array T, because the rare "product of the others"
+//              branch re-reads every t while E is overwritten in place.
 //   vn_kernel  one workgroup (16 wavefronts) per tile; wavefront w takes
 //              columns w, w+16, ...:
 //                L = ch + ((0+E[r0])+E[r1])+...  rows ascending (:173-185)
@@ -46,6 +48,7 @@ constexpr double kCL = 0.99999999999999878;  // spa_decoder.py:141,167
 constexpr double kTiny = 1e-10;              // spa_decoder.py:159
 constexpr int kCnRowsPerBlock = 4;           // 4 wavefronts = 4 rows of one tile
 constexpr int kVnWaves = 16;                 // wavefronts per VN workgroup
+constexpr int kPv = 4;                       // VN column-sum loads in flight
 
 __device__ __forceinline__ int uniform(int x) { return __builtin_amdgcn_readfirstlane(x); }
 
@@ -90,6 +93,34 @@ __device__ __forceinline__ double cn_tanh(double M, const LdsTanh &t) {
 }
 
 // --------------------------------------------------------------- CN pass
+constexpr int kPf = 4;  // edges in flight per wavefront (software pipeline depth)
+
+// Register ring of the next kPf edges' (L[col], E_old) loads.  take(k, e)
+// returns M for edge e (ring slot k) and issues the loads for edge e + kPf.
+template <bool kFirst>
+struct EdgeStream {
+    const DevGraph &g;
+    const double *Lt, *Et;
+    int end;
+    double lv[kPf], eo[kPf];
+    __device__ __forceinline__ EdgeStream(const DevGraph &g_, const double *L_, const double *E_, int beg, int end_)
+        : g(g_), Lt(L_), Et(E_), end(end_) {
+#pragma unroll
+        for (int k = 0; k < kPf; ++k) fetch(k, beg + k);
+    }
+    __device__ __forceinline__ void fetch(int k, int e) {
+        // unconditional (index clamped into the row): no phi, so the compiler
+        // keeps the ring in place and waits only for the slot it consumes
+        const int i = e < end ? e : end - 1;
+        lv[k] = Lt[g.col_idx[i] * kTile];
+        eo[k] = kFirst ? 0.0 : Et[i * kTile];
+    }
+    __device__ __forceinline__ double take(int k, int e) {
+        const double M = kFirst ? lv[k] : lv[k] - eo[k];
+        fetch(k, e + kPf);
+        return M;
+    }
+};
 template <bool kFirst>
 __global__ __launch_bounds__(256) void cn_kernel(DevGraph g, DevState st, int blocks_per_tile) {
     __shared__ MathLds mlds;
@@ -117,21 +148,56 @@ __global__ __launch_bounds__(256) void cn_kernel(DevGraph g, DevState st, int bl
     double *Tt = st.T + (size_t)tile * g.nnz * kTile + lane;
     const double *Lt = (kFirst ? st.ch : st.L) + (size_t)tile * g.n * kTile + lane;
 
+    // Both passes stream (L[col], E_old) through a register ring of kPf
+    // edges, so kPf edges' loads are in flight per wavefront.
+    // pass 1: P = t0*t1*... left to right; nothing is stored
     double P = 1.0;
+    bool tiny = false;
+    {
+        EdgeStream<kFirst> es(g, Lt, Et, beg, end);
+        for (int e = beg; e < end; e += kPf) {
+#pragma unroll
+            for (int k = 0; k < kPf; ++k) {
+                const double M = es.take(k, e + k);
+                if (e + k < end) {  // wave-uniform
+                    const double t = cn_tanh(M, ttab);
+                    P = (e + k == beg) ? t : P * t;
+                    tiny |= !(fabs(t) > kTiny);
+                }
+            }
+        }
+    }
+    if (__ballot(tiny) == 0ull) {
+        // pass 2: recompute t from the same E_old / L bits (identical result),
+        // E_new = 2 atanh(clip(P/t)) written over E_old.  24 B of HBM per edge
+        // instead of parking t (32 B).
+        EdgeStream<kFirst> es(g, Lt, Et, beg, end);
+        for (int e = beg; e < end; e += kPf) {
+#pragma unroll
+            for (int k = 0; k < kPf; ++k) {
+                const double M = es.take(k, e + k);
+                if (e + k < end) {  // wave-uniform
+                    const double t = cn_tanh(M, ttab);
+                    const double En = 2.0 * atanh_f(clip_cl(P / t), ltab);
+                    if (live) Et[(e + k) * kTile] = En;
+                }
+            }
+        }
+        return;
+    }
+    // Rare (some |t| <= 1e-10 in this wavefront): "product of the others" needs
+    // every t of the row while E is being overwritten -> park t in T first.
     for (int e = beg; e < end; ++e) {
-        const int c = g.col_idx[e];
-        double M = Lt[c * kTile];
+        double M = Lt[g.col_idx[e] * kTile];
         if (!kFirst) M = M - Et[e * kTile];
-        const double t = cn_tanh(M, ttab);
-        P = (e == beg) ? t : P * t;
-        Tt[e * kTile] = t;
+        Tt[e * kTile] = cn_tanh(M, ttab);
     }
     for (int e = beg; e < end; ++e) {
         const double t = Tt[e * kTile];
         double q;
         if (fabs(t) > kTiny) {
             q = P / t;
-        } else {  // np.prod(np.delete(tanh_array, idx)): rare, re-walk the row
+        } else {  // np.prod(np.delete(tanh_array, idx)) (spa_decoder.py:164)
             q = 1.0;
             bool first = true;
             for (int e2 = beg; e2 < end; ++e2) {
@@ -170,8 +236,21 @@ __global__ __launch_bounds__(1024) void vn_kernel(DevGraph g, DevState st, int i
     int my_cnt = 0;
     for (int j = wave; j < g.n; j += nwaves) {
         const int p0 = g.csc_ptr[j], p1 = g.csc_ptr[j + 1];
-        double s = 0.0;  // scipy csr_matvec: sum starts at y[i] = 0
-        for (int p = p0; p < p1; ++p) s = s + Et[g.csc_edge[p] * kTile];
+        double s = 0.0;  // scipy csr_matvec: sum starts at y[i] = 0, rows ascending
+        {
+            // ring of kPv loads in flight (indices clamped into the column)
+            double ring[kPv];
+#pragma unroll
+            for (int k = 0; k < kPv; ++k) ring[k] = Et[g.csc_edge[min(p0 + k, p1 - 1)] * kTile];
+            for (int p = p0; p < p1; p += kPv) {
+#pragma unroll
+                for (int k = 0; k < kPv; ++k) {
+                    const double v = ring[k];
+                    ring[k] = Et[g.csc_edge[min(p + k + kPv, p1 - 1)] * kTile];
+                    if (p + k < p1) s = s + v;
+                }
+            }
+        }
         const double chj = Ct[j * kTile];
         const double Lj = chj + s;  // channel added after the sum (:173,185)
         if (nllr && j < g.k) {
