@@ -88,6 +88,22 @@ def max_over_ranks(dist, x, local):
     return float(t.item())
 
 
+def committed_traffic(nnz, frames):
+    """HBM bytes per cn_kernel launch from the newest committed PMC pass
+    (profiles/*/traffic.json, tools/profile.sh + tools/summarize_profile.py)
+    for this exact workload shape, or (None, None)."""
+    pdir = os.path.join(ROOT, "profiles")
+    best = None
+    for d in sorted(os.listdir(pdir)) if os.path.isdir(pdir) else []:
+        f = os.path.join(pdir, d, "traffic.json")
+        if not os.path.exists(f):
+            continue
+        t = json.load(open(f))
+        if t.get("edges") == nnz and t.get("frames") == frames:
+            best = (t["kernels"]["cn_kernel<false>"]["traffic_bytes"], os.path.relpath(f, ROOT))
+    return best or (None, None)
+
+
 def cpu_baseline(H, k, args):
     """The C oracle (oracle/spa_oracle.c, OpenMP over frames) on a bounded
     sample of the same workload; frames from the oracle's restatement of the
@@ -133,9 +149,13 @@ def main():
     sigma = 1.0 / math.sqrt(2.0 * 1.0 * (10.0 ** (args.snr * 0.1)))  # channel.py:113
     B = args.frames
 
-    def step(s):
-        frame0 = (s * world + rank) * B
+    local_totals = np.zeros((1, 7), np.int64)
+
+    def step(s, record=False):
+        frame0 = (s * world + rank) * B  # disjoint global frame ranges per rank and step
         c = dec.mc_run(SEED, [sigma], B, frame0, args.iters)
+        if record:
+            local_totals[:] += c
         return allreduce_counters(dist, c, local)
 
     for s in range(args.warmup):
@@ -147,7 +167,7 @@ def main():
     t0 = time.perf_counter()
     totals = np.zeros((1, 7), np.int64)
     for s in range(args.steps):
-        totals += step(args.warmup + s)
+        totals += step(args.warmup + s, record=True)
     barrier(dist, local)
     elapsed = time.perf_counter() - t0
     dec.profile(False)
@@ -163,7 +183,7 @@ def main():
     # bytes = 16 B per edge per frame-iteration (read E_old + write E_new)
     cn_ms, cn_launches = prof["cn"]
     vn_ms, vn_launches = prof["vn"]
-    local_iters = iters_total // world  # frames per rank are statistically identical
+    local_iters = int(local_totals[0, 6])  # this rank's frame-iterations
     cn_bytes_total = 16.0 * nnz * local_iters
     cn_avg_s = (cn_ms / 1e3) / max(cn_launches, 1)
     cn_bytes_per_launch = cn_bytes_total / max(cn_launches, 1)
@@ -173,6 +193,7 @@ def main():
     frames_local = B * args.steps
     dec_bytes = frames_local * (8 * n + math.ceil(n / 8) + 8) + 16.0 * nnz * local_iters
     decode_gbs = dec_bytes / (decode_ms / 1e3) / 1e9 if decode_ms else 0.0
+    traffic, traffic_src = committed_traffic(nnz, chunk)
 
     out = {
         "metric": METRIC,
@@ -201,7 +222,7 @@ def main():
         "avg_iters": iters_total / frames_total,
         "roofline": {
             "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+            "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
             "kernel": "cn_kernel", "launches": cn_launches, "avg_launch_ms": cn_avg_s * 1e3,
             "bytes_per_launch": cn_bytes_per_launch,
             "bytes_model": "16 B x H_std edges x frame-iterations executed (E_old read + E_new write)",

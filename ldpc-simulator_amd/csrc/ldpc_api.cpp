@@ -51,6 +51,8 @@ struct ldpc_decoder {
     const ldpc_graph *g = nullptr;
     int cap_tiles = 0;
     double *E = nullptr, *T = nullptr, *L = nullptr, *ch = nullptr;
+    int *rare = nullptr;  // rare_count[2] + rare_list[cap_tiles*m]
+    int nslots = 0;
     int *ints = nullptr;  // done, conv, status, iters, nllr_cnt (cap frames each) + tile_active
     uint32_t *ubits = nullptr;
     // staging for host I/O
@@ -106,6 +108,9 @@ void state_bind(ldpc_decoder *d, int ntiles, int count) {
     DevState &s = d->st;
     s.E = d->E;
     s.T = d->T;
+    s.rare_count = d->rare;
+    s.rare_list = d->rare + 2;
+    s.nslots = d->nslots;
     s.L = d->L;
     s.ch = d->ch;
     s.done = d->ints;
@@ -149,17 +154,23 @@ hipError_t run_iterations(ldpc_decoder *d, const DevGraph &G, const DevState &st
     hipError_t e = hipSuccess;
     for (int it = 0; it < max_iter && e == hipSuccess; ++it) {
         e = timed(d, LDPC_K_CN, s, [&] { return ldpc::launch_cn(G, st, it, s); });
+        if (e == hipSuccess) e = ldpc::launch_cn_rare(G, st, it, s);
         if (e == hipSuccess)
             e = timed(d, LDPC_K_VN, s, [&] { return ldpc::launch_vn(G, st, it, max_iter, nllr, s); });
     }
     return e;
 }
 
+// cn_rare_kernel runs 1024 blocks x 4 wavefronts; one scratch slot each.
+int scratch_slots() { return 4096; }
+
 size_t workspace_bytes(const DevGraph &g, int cap_tiles) {
     const size_t cap = (size_t)cap_tiles * kTile;
     const size_t kw = (size_t)((g.k + 31) / 32);
     size_t b = 0;
-    b += 2 * cap * (size_t)g.nnz * 8;  // E, T
+    b += cap * (size_t)g.nnz * 8;                                   // E
+    b += (size_t)scratch_slots() * g.max_row_deg * kTile * 8;            // T pool
+    b += 4 * (2 + (size_t)cap_tiles * g.m);                               // rare list
     b += 2 * cap * (size_t)g.n * 8;    // L, ch
     b += (5 * cap + cap_tiles) * 4;    // per-frame ints + tile flags
     b += cap * kw * 4;                 // ubits
@@ -315,7 +326,11 @@ int ldpc_decoder_create(const ldpc_graph *g, int32_t max_frames, ldpc_decoder **
     const size_t kw = (size_t)((G.k + 31) / 32);
     int rc = LDPC_OK;
     if (!rc) rc = dev_alloc(&d->E, cap * (size_t)G.nnz);
-    if (!rc) rc = dev_alloc(&d->T, cap * (size_t)G.nnz);
+    d->nslots = scratch_slots();
+    if (!rc) rc = dev_alloc(&d->T, (size_t)d->nslots * G.max_row_deg * kTile);
+    if (!rc) rc = dev_alloc(&d->rare, 2 + (size_t)d->cap_tiles * G.m);
+    if (!rc && hipMemset(d->rare, 0, sizeof(int) * 2) != hipSuccess)
+        rc = ldpc_fail(LDPC_EDEVICE, "ldpc_decoder_create: memset failed");
     if (!rc) rc = dev_alloc(&d->L, cap * (size_t)G.n);
     if (!rc) rc = dev_alloc(&d->ch, cap * (size_t)G.n);
     if (!rc) rc = dev_alloc(&d->ints, 5 * cap + (size_t)d->cap_tiles);
@@ -336,6 +351,7 @@ int ldpc_decoder_destroy(ldpc_decoder *d) {
     DeviceGuard dg(d->g ? d->g->device : -1);
     (void)hipFree(d->E);
     (void)hipFree(d->T);
+    (void)hipFree(d->rare);
     (void)hipFree(d->L);
     (void)hipFree(d->ch);
     (void)hipFree(d->ints);

@@ -6,7 +6,8 @@
 // 64 consecutive doubles (512 contiguous bytes): fully coalesced, with no
 // index math per lane.
 //   E   [tile][nnz][64]  fp64 check->variable messages (CSR edge order of H_std)
-//   T   [tile][nnz][64]  fp64 scratch: tanh(M/2) parked between the CN passes
+//   T   [slot][max_row_deg][64] fp64 scratch of cn_rare_kernel (slot = its
+//                        global wavefront id; nslots = 4 x its grid)
 //   L   [tile][n][64]    fp64 a-posteriori LLRs
 //   ch  [tile][n][64]    fp64 channel LLRs
 //   ub  [tile][kw][64]   info bits (Monte-Carlo path), kw = ceil(k/32)
@@ -34,6 +35,9 @@ struct DevState {
     double *E, *T, *L, *ch;
     int *done, *conv, *status, *iters, *nllr_cnt;
     int *tile_active;
+    int *rare_list;          // [ntiles*m] tile*m+row of rows left to cn_rare_kernel
+    int *rare_count;         // [2] per iteration parity
+    int nslots;
     uint32_t *ubits;         // MC only (may be null)
     double *nllr_hist;       // [frame][hist_stride] or null
     int hist_stride;
@@ -45,6 +49,7 @@ struct DevState {
 hipError_t launch_reset(const DevGraph &g, const DevState &st, hipStream_t s);
 hipError_t launch_load_llr(const DevGraph &g, const DevState &st, const double *llr, hipStream_t s);
 hipError_t launch_cn(const DevGraph &g, const DevState &st, int it, hipStream_t s);
+hipError_t launch_cn_rare(const DevGraph &g, const DevState &st, int it, hipStream_t s);
 hipError_t launch_vn(const DevGraph &g, const DevState &st, int it, int max_iter, bool nllr, hipStream_t s);
 hipError_t launch_finalize(const DevGraph &g, const DevState &st, uint8_t *z, double *post,
                            hipStream_t s);

@@ -93,18 +93,25 @@ __device__ __forceinline__ double cn_tanh(double M, const LdsTanh &t) {
 }
 
 // --------------------------------------------------------------- CN pass
-constexpr int kPf = 4;  // edges in flight per wavefront (software pipeline depth)
+#ifndef LDPC_CN_WAVES
+#define LDPC_CN_WAVES 7  // min wavefronts per SIMD for cn_kernel (register budget)
+#endif
+#ifndef LDPC_PF
+#define LDPC_PF 4
+#endif
+constexpr int kPf = LDPC_PF;  // edges in flight per wavefront (software pipeline depth)
 
 // Register ring of the next kPf edges' (L[col], E_old) loads.  take(k, e)
 // returns M for edge e (ring slot k) and issues the loads for edge e + kPf.
 template <bool kFirst>
 struct EdgeStream {
-    const DevGraph &g;
+    const int *__restrict__ col;
     const double *Lt, *Et;
     int end;
     double lv[kPf], eo[kPf];
-    __device__ __forceinline__ EdgeStream(const DevGraph &g_, const double *L_, const double *E_, int beg, int end_)
-        : g(g_), Lt(L_), Et(E_), end(end_) {
+    __device__ __forceinline__ EdgeStream(const int *__restrict__ col_, const double *L_, const double *E_, int beg,
+                                          int end_)
+        : col(col_), Lt(L_), Et(E_), end(end_) {
 #pragma unroll
         for (int k = 0; k < kPf; ++k) fetch(k, beg + k);
     }
@@ -112,7 +119,7 @@ struct EdgeStream {
         // unconditional (index clamped into the row): no phi, so the compiler
         // keeps the ring in place and waits only for the slot it consumes
         const int i = e < end ? e : end - 1;
-        lv[k] = Lt[g.col_idx[i] * kTile];
+        lv[k] = Lt[col[i] * kTile];  // col[] is read-only + noalias -> scalar load
         eo[k] = kFirst ? 0.0 : Et[i * kTile];
     }
     __device__ __forceinline__ double take(int k, int e) {
@@ -122,7 +129,9 @@ struct EdgeStream {
     }
 };
 template <bool kFirst>
-__global__ __launch_bounds__(256) void cn_kernel(DevGraph g, DevState st, int blocks_per_tile) {
+__global__ __launch_bounds__(256, LDPC_CN_WAVES) void cn_kernel(DevGraph g, DevState st, int blocks_per_tile,
+                                                                int it_parity, const int *__restrict__ col_idx,
+                                                                const int *__restrict__ row_ptr) {
     __shared__ MathLds mlds;
     fill_math_lds(mlds);
     __syncthreads();
@@ -139,13 +148,12 @@ __global__ __launch_bounds__(256) void cn_kernel(DevGraph g, DevState st, int bl
     const int row = (slot % blocks_per_tile) * kCnRowsPerBlock + wave;
     if (tile >= st.ntiles || row >= g.m) return;
     if (!st.tile_active[tile]) return;
-    const int beg = g.row_ptr[row], end = g.row_ptr[row + 1];
+    const int beg = row_ptr[row], end = row_ptr[row + 1];
     if (beg == end) return;  // spa_decoder.py:115-122
 
     const int f = tile * kTile + lane;
     const bool live = st.done[f] == 0;
     double *Et = st.E + (size_t)tile * g.nnz * kTile + lane;
-    double *Tt = st.T + (size_t)tile * g.nnz * kTile + lane;
     const double *Lt = (kFirst ? st.ch : st.L) + (size_t)tile * g.n * kTile + lane;
 
     // Both passes stream (L[col], E_old) through a register ring of kPf
@@ -154,7 +162,7 @@ __global__ __launch_bounds__(256) void cn_kernel(DevGraph g, DevState st, int bl
     double P = 1.0;
     bool tiny = false;
     {
-        EdgeStream<kFirst> es(g, Lt, Et, beg, end);
+        EdgeStream<kFirst> es(col_idx, Lt, Et, beg, end);
         for (int e = beg; e < end; e += kPf) {
 #pragma unroll
             for (int k = 0; k < kPf; ++k) {
@@ -171,7 +179,7 @@ __global__ __launch_bounds__(256) void cn_kernel(DevGraph g, DevState st, int bl
         // pass 2: recompute t from the same E_old / L bits (identical result),
         // E_new = 2 atanh(clip(P/t)) written over E_old.  24 B of HBM per edge
         // instead of parking t (32 B).
-        EdgeStream<kFirst> es(g, Lt, Et, beg, end);
+        EdgeStream<kFirst> es(col_idx, Lt, Et, beg, end);
         for (int e = beg; e < end; e += kPf) {
 #pragma unroll
             for (int k = 0; k < kPf; ++k) {
@@ -185,36 +193,74 @@ __global__ __launch_bounds__(256) void cn_kernel(DevGraph g, DevState st, int bl
         }
         return;
     }
-    // Rare (some |t| <= 1e-10 in this wavefront): "product of the others" needs
-    // every t of the row while E is being overwritten -> park t in T first.
-    for (int e = beg; e < end; ++e) {
-        double M = Lt[g.col_idx[e] * kTile];
-        if (!kFirst) M = M - Et[e * kTile];
-        Tt[e * kTile] = cn_tanh(M, ttab);
+    // Rare: some |t| <= 1e-10 in this wavefront.  Leave E untouched and hand
+    // the row to cn_rare_kernel (next launch), which needs every t of the row
+    // while overwriting E and so parks them in a scratch slot.
+    if (lane == 0) {
+        const int at = atomicAdd(&st.rare_count[it_parity], 1);
+        st.rare_list[at] = tile * g.m + row;
     }
-    for (int e = beg; e < end; ++e) {
-        const double t = Tt[e * kTile];
-        double q;
-        if (fabs(t) > kTiny) {
-            q = P / t;
-        } else {  // np.prod(np.delete(tanh_array, idx)) (spa_decoder.py:164)
-            q = 1.0;
-            bool first = true;
-            for (int e2 = beg; e2 < end; ++e2) {
-                if (e2 == e) continue;
-                const double t2 = Tt[e2 * kTile];
-                q = first ? t2 : q * t2;
-                first = false;
-            }
+}
+
+// Rows recorded by cn_kernel: same update, with t parked in this wavefront's
+// own scratch slot (slot = global wavefront id; grid-stride over the list).
+template <bool kFirst>
+__global__ __launch_bounds__(256) void cn_rare_kernel(DevGraph g, DevState st, int it_parity) {
+    __shared__ MathLds mlds;
+    const int count = st.rare_count[it_parity];
+    if (blockIdx.x == 0 && threadIdx.x == 0) st.rare_count[it_parity ^ 1] = 0;  // for the next CN
+    if (count == 0) return;  // block-uniform
+    fill_math_lds(mlds);
+    __syncthreads();
+    const LdsTanh ttab{mlds.tanh};
+    const LdsLog ltab{mlds.log};
+    const int lane = threadIdx.x & 63;
+    const int gw = (int)blockIdx.x * 4 + uniform(threadIdx.x >> 6);
+    const int nw = (int)gridDim.x * 4;
+    double *Tt = st.T + (size_t)gw * g.max_row_deg * kTile + lane;
+    for (int idx = gw; idx < count; idx += nw) {
+        const int code = st.rare_list[idx];
+        const int tile = code / g.m, row = code % g.m;
+        const int beg = g.row_ptr[row], end = g.row_ptr[row + 1];
+        const int f = tile * kTile + lane;
+        const bool live = st.done[f] == 0;
+        double *Et = st.E + (size_t)tile * g.nnz * kTile + lane;
+        const double *Lt = (kFirst ? st.ch : st.L) + (size_t)tile * g.n * kTile + lane;
+        double P = 1.0;
+        for (int e = beg; e < end; ++e) {
+            double M = Lt[g.col_idx[e] * kTile];
+            if (!kFirst) M = M - Et[e * kTile];
+            const double t = cn_tanh(M, ttab);
+            P = (e == beg) ? t : P * t;
+            Tt[(e - beg) * kTile] = t;
         }
-        const double En = 2.0 * atanh_f(clip_cl(q), ltab);
-        if (live) Et[e * kTile] = En;
+        for (int e = beg; e < end; ++e) {
+            const double t = Tt[(e - beg) * kTile];
+            double q;
+            if (fabs(t) > kTiny) {
+                q = P / t;
+            } else {  // np.prod(np.delete(tanh_array, idx)) (spa_decoder.py:164)
+                q = 1.0;
+                bool first = true;
+                for (int e2 = beg; e2 < end; ++e2) {
+                    if (e2 == e) continue;
+                    const double t2 = Tt[(e2 - beg) * kTile];
+                    q = first ? t2 : q * t2;
+                    first = false;
+                }
+            }
+            const double En = 2.0 * atanh_f(clip_cl(q), ltab);
+            if (live) Et[e * kTile] = En;
+        }
     }
 }
 
 // ------------------------------------------------------- VN + syndrome pass
 template <bool kFirst>
-__global__ __launch_bounds__(1024) void vn_kernel(DevGraph g, DevState st, int it, int last, int nllr) {
+__global__ __launch_bounds__(1024) void vn_kernel(DevGraph g, DevState st, int it, int last, int nllr,
+                                                  const int *__restrict__ csc_ptr,
+                                                  const int *__restrict__ csc_edge,
+                                                  const int *__restrict__ csc_row) {
     extern __shared__ uint32_t par[];  // [mw][64] row parities of z^1, one column per frame
     __shared__ int cnt_lds[kTile];
     const int tile = blockIdx.x;
@@ -235,18 +281,18 @@ __global__ __launch_bounds__(1024) void vn_kernel(DevGraph g, DevState st, int i
 
     int my_cnt = 0;
     for (int j = wave; j < g.n; j += nwaves) {
-        const int p0 = g.csc_ptr[j], p1 = g.csc_ptr[j + 1];
+        const int p0 = csc_ptr[j], p1 = csc_ptr[j + 1];
         double s = 0.0;  // scipy csr_matvec: sum starts at y[i] = 0, rows ascending
         {
             // ring of kPv loads in flight (indices clamped into the column)
             double ring[kPv];
 #pragma unroll
-            for (int k = 0; k < kPv; ++k) ring[k] = Et[g.csc_edge[min(p0 + k, p1 - 1)] * kTile];
+            for (int k = 0; k < kPv; ++k) ring[k] = Et[csc_edge[min(p0 + k, p1 - 1)] * kTile];
             for (int p = p0; p < p1; p += kPv) {
 #pragma unroll
                 for (int k = 0; k < kPv; ++k) {
                     const double v = ring[k];
-                    ring[k] = Et[g.csc_edge[min(p + k + kPv, p1 - 1)] * kTile];
+                    ring[k] = Et[csc_edge[min(p + k + kPv, p1 - 1)] * kTile];
                     if (p + k < p1) s = s + v;
                 }
             }
@@ -260,7 +306,7 @@ __global__ __launch_bounds__(1024) void vn_kernel(DevGraph g, DevState st, int i
         if (live) Lt[j * kTile] = Lj;
         if (!(Lj < 0.0)) {  // z^1 == 1 -> flips the parity of every row of column j
             for (int p = p0; p < p1; ++p) {
-                const int r = g.csc_row[p];
+                const int r = csc_row[p];
                 atomicXor(&par[(r >> 5) * kTile + lane], 1u << (r & 31));
             }
         }
@@ -486,10 +532,21 @@ hipError_t launch_load_llr(const DevGraph &g, const DevState &st, const double *
 hipError_t launch_cn(const DevGraph &g, const DevState &st, int it, hipStream_t s) {
     const int bpt = (g.m + kCnRowsPerBlock - 1) / kCnRowsPerBlock;
     const unsigned grid = (unsigned)(((st.ntiles + 7) / 8) * 8 * bpt);
+    const int par = it & 1;
     if (it == 0)
-        cn_kernel<true><<<grid, 256, 0, s>>>(g, st, bpt);
+        cn_kernel<true><<<grid, 256, 0, s>>>(g, st, bpt, par, g.col_idx, g.row_ptr);
     else
-        cn_kernel<false><<<grid, 256, 0, s>>>(g, st, bpt);
+        cn_kernel<false><<<grid, 256, 0, s>>>(g, st, bpt, par, g.col_idx, g.row_ptr);
+    return hipGetLastError();
+}
+
+hipError_t launch_cn_rare(const DevGraph &g, const DevState &st, int it, hipStream_t s) {
+    const unsigned grid = (unsigned)(st.nslots / 4);
+    const int par = it & 1;
+    if (it == 0)
+        cn_rare_kernel<true><<<grid, 256, 0, s>>>(g, st, par);
+    else
+        cn_rare_kernel<false><<<grid, 256, 0, s>>>(g, st, par);
     return hipGetLastError();
 }
 
@@ -497,9 +554,11 @@ hipError_t launch_vn(const DevGraph &g, const DevState &st, int it, int max_iter
     const size_t lds = (size_t)((g.m + 31) >> 5) * kTile * sizeof(uint32_t);
     const int last = it == max_iter - 1 ? 1 : 0;
     if (it == 0)
-        vn_kernel<true><<<st.ntiles, kVnWaves * 64, lds, s>>>(g, st, it, last, nllr ? 1 : 0);
+        vn_kernel<true><<<st.ntiles, kVnWaves * 64, lds, s>>>(g, st, it, last, nllr ? 1 : 0, g.csc_ptr, g.csc_edge,
+                                                               g.csc_row);
     else
-        vn_kernel<false><<<st.ntiles, kVnWaves * 64, lds, s>>>(g, st, it, last, nllr ? 1 : 0);
+        vn_kernel<false><<<st.ntiles, kVnWaves * 64, lds, s>>>(g, st, it, last, nllr ? 1 : 0, g.csc_ptr, g.csc_edge,
+                                                                g.csc_row);
     return hipGetLastError();
 }
 

@@ -70,11 +70,13 @@ struct LogEntry {
 // interval holding 1.0 itself is exact: invc = 1), which is all atanh needs.
 template <class LogTab>
 __host__ __device__ __forceinline__ void log_hilo(double x, const LogTab &lt, double &hi, double &lo) {
+    // glibc-style reduction on the high word only (the offset's low word is 0,
+    // so no borrow): tmp = hi(x) - hi(OFF); 32-bit integer ops throughout.
     const uint64_t ix = dbits(x);
-    const uint64_t tmp = ix - 0x3fe6000000000000ull;
-    const int i = (int)((tmp >> 45) & 127);
-    const int k = (int)((int64_t)tmp >> 52);
-    const double z = dfrom(ix - (tmp & (0xfffull << 52)));
+    const int tmp = (int)(uint32_t)(ix >> 32) - 0x3fe60000;
+    const int i = (tmp >> 13) & 127;
+    const int k = tmp >> 20;  // arithmetic shift
+    const double z = dfrom(ix - ((uint64_t)(uint32_t)(tmp & 0xfff00000) << 32));
     const LogEntry t = lt(i);
     const double r = __builtin_fma(z, t.invc, -1.0);  // |r| < 2^-7
     const double kd = (double)k;

@@ -78,3 +78,20 @@ def test_mc_sharding_is_additive(gpu_available):
     a = dec.mc_run(SEED, sig, 128, 0, 8)
     b = dec.mc_run(SEED, sig, 128, 128, 8)
     np.testing.assert_array_equal(whole, a + b)
+
+
+def test_simulate_end_to_end_results_schema(gpu_available, tmp_path):
+    """montecarlo.simulate: GPU sweep -> reference results schema, counters == oracle."""
+    from ldpc_amd import montecarlo as mc
+    from ldpc_amd.results import SimulationResult
+    snrs = mc.snr_grid(0.0, 2.0, 1.0)
+    res, ctr = mc.simulate("BCH_7_4_1_strip", snrs, 2000, 10)
+    H = hstd_for("BCH_7_4_1_strip")
+    for p, s in enumerate(snrs):
+        u, _, llr = oracle.generate_frames(H, SEED, p, mc.sigma_for_snr(s), 0, 2000)
+        o = oracle.spa_decode(H, llr, 10)
+        want = oracle.main_counters(u, o["z"], o["status"], o["conv"], iters=o["iters"])
+        np.testing.assert_array_equal(ctr[p][[0, 1, 2, 3, 4, 6]], want[[0, 1, 2, 3, 4, 6]])
+    res.to_json(tmp_path / "r.json")
+    back = SimulationResult.from_json(tmp_path / "r.json")
+    assert [sp.fer for sp in back.snr_points] == [sp.fer for sp in res.snr_points]

@@ -1,0 +1,60 @@
+#!/usr/bin/env python3
+"""Summarize a tools/profile.sh run into profiles/<tag>/ (committed evidence).
+
+Writes kernel_stats.csv (rocprofv3 --stats, verbatim), pmc_summary.csv (mean
+FETCH_SIZE / WRITE_SIZE per kernel, KiB as rocprofv3 reports them) and
+traffic.json: HBM bytes per launch of each kernel, corrected as
+MI355X_MICROARCH.md §HBM prescribes -- FETCH_SIZE on gfx950 tallies 64 B per
+128-B request, so reads are doubled; the factor is re-derived here from the
+VN kernel, whose algorithmic read (each message once) is known exactly.
+"""
+import collections
+import csv
+import json
+import os
+import shutil
+import sys
+
+
+def main(src, dst, nnz, frames):
+    os.makedirs(dst, exist_ok=True)
+    shutil.copy(os.path.join(src, "trace", "run_kernel_stats.csv"), os.path.join(dst, "kernel_stats.csv"))
+    agg = collections.defaultdict(dict)
+    for name, sub in (("FETCH_SIZE", "pmc_fetch"), ("WRITE_SIZE", "pmc_write")):
+        vals = collections.defaultdict(list)
+        for r in csv.DictReader(open(os.path.join(src, sub, "run_counter_collection.csv"))):
+            vals[r["Kernel_Name"]].append(float(r["Counter_Value"]))
+        for k, v in vals.items():
+            agg[k][name] = sum(v) / len(v)
+            agg[k]["dispatches"] = len(v)
+    with open(os.path.join(dst, "pmc_summary.csv"), "w", newline="") as fh:
+        w = csv.writer(fh)
+        w.writerow(["kernel", "dispatches", "FETCH_SIZE_KiB_mean", "WRITE_SIZE_KiB_mean"])
+        for k, v in sorted(agg.items()):
+            w.writerow([k, v.get("dispatches"), v.get("FETCH_SIZE"), v.get("WRITE_SIZE")])
+    stats = {r["Name"]: r for r in csv.DictReader(open(os.path.join(dst, "kernel_stats.csv")))}
+
+    def find(prefix, table):
+        for k in table:
+            if prefix in k:
+                return k
+        raise KeyError(prefix)
+
+    vn = find("vn_kernel<false>", agg)
+    vn_alg = 8.0 * nnz * frames  # each message read once
+    factor = vn_alg / (agg[vn]["FETCH_SIZE"] * 1024.0)
+    out = {"fetch_correction_factor": factor, "frames": frames, "edges": nnz, "kernels": {}}
+    for key in ("cn_kernel<false>", "vn_kernel<false>"):
+        k = find(key, agg)
+        rd = agg[k]["FETCH_SIZE"] * 1024.0 * factor
+        wr = agg[k]["WRITE_SIZE"] * 1024.0
+        s = stats[find(key, stats)]
+        out["kernels"][key] = {"read_bytes": rd, "write_bytes": wr, "traffic_bytes": rd + wr,
+                               "avg_ns": float(s["AverageNs"]), "calls": int(s["Calls"]),
+                               "traffic_GBs": (rd + wr) / float(s["AverageNs"])}
+    json.dump(out, open(os.path.join(dst, "traffic.json"), "w"), indent=2)
+    print(json.dumps(out, indent=2))
+
+
+if __name__ == "__main__":
+    main(sys.argv[1], sys.argv[2], int(sys.argv[3]), int(sys.argv[4]))
