@@ -46,6 +46,9 @@ def parse():
     ap.add_argument("--snr", type=float, default=0.0, help="reference SNR axis (dB), speed=1")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU-baseline sample budget (0 = skip)")
     ap.add_argument("--cpu-threads", type=int, default=0)
+    ap.add_argument("--dist-backend", default="nccl",
+                    help="torch.distributed backend for N>1 ('nccl' = RCCL over xGMI; 'gloo' for "
+                         "rehearsing several ranks on one GPU)")
     return ap.parse_args()
 
 
@@ -54,12 +57,18 @@ def dist_setup(args):
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
+    device = local
     if world > 1:
         import torch
         import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl")  # RCCL on ROCm
-    return world, rank, local, dist
+        device = local % max(1, torch.cuda.device_count())
+        torch.cuda.set_device(device)
+        dist.init_process_group(args.dist_backend)  # "nccl" is RCCL on ROCm
+    return world, rank, device, dist
+
+
+def _dev(dist, local):
+    return "cpu" if dist.get_backend() == "gloo" else f"cuda:{local}"
 
 
 def allreduce_counters(dist, ctr, local):
@@ -67,7 +76,7 @@ def allreduce_counters(dist, ctr, local):
     if dist is None:
         return ctr
     import torch
-    t = torch.from_numpy(ctr.reshape(-1).copy()).to(f"cuda:{local}")
+    t = torch.from_numpy(ctr.reshape(-1).copy()).to(_dev(dist, local))
     dist.all_reduce(t)
     return t.cpu().numpy().reshape(ctr.shape)
 
@@ -76,14 +85,15 @@ def barrier(dist, local):
     if dist is not None:
         import torch
         dist.barrier()
-        torch.cuda.synchronize(local)
+        if torch.cuda.is_available():
+            torch.cuda.synchronize(local)
 
 
 def max_over_ranks(dist, x, local):
     if dist is None:
         return x
     import torch
-    t = torch.tensor([x], dtype=torch.float64, device=f"cuda:{local}")
+    t = torch.tensor([x], dtype=torch.float64, device=_dev(dist, local))
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
 

@@ -37,6 +37,7 @@
 
 #include <cmath>
 #include <cstdint>
+#include <cstdlib>
 
 #include "spa_device.h"
 #include "spa_math.h"
@@ -89,6 +90,9 @@ __device__ __forceinline__ void fill_math_lds(MathLds &m) {
 
 __device__ __forceinline__ double cn_tanh(double M, const LdsTanh &t) {
     const double d = M * 0.5;  // == M/2.0 bit for bit (power-of-two scale)
+#ifdef LDPC_DIAG_NOMATH  // diagnostic build only: memory pattern without the math
+    return d * 0.25 + 0.5;
+#endif
     return d > 17.5 ? kCL : (d < -17.5 ? -kCL : np_tanh(d, t));
 }
 
@@ -99,6 +103,15 @@ __device__ __forceinline__ double cn_tanh(double M, const LdsTanh &t) {
 #ifndef LDPC_PF
 #define LDPC_PF 4
 #endif
+// Tuning knob (experiments only): LDPC_CN_LDS_PAD=<bytes> of dynamic LDS per
+// cn_kernel block caps its blocks per CU (occupancy) without a rebuild.
+inline size_t cn_lds_pad() {
+    static const size_t pad = [] {
+        const char *e = getenv("LDPC_CN_LDS_PAD");
+        return e ? (size_t)strtoul(e, nullptr, 10) : (size_t)0;
+    }();
+    return pad;
+}
 constexpr int kPf = LDPC_PF;  // edges in flight per wavefront (software pipeline depth)
 
 // Register ring of the next kPf edges' (L[col], E_old) loads.  take(k, e)
@@ -186,7 +199,11 @@ __global__ __launch_bounds__(256, LDPC_CN_WAVES) void cn_kernel(DevGraph g, DevS
                 const double M = es.take(k, e + k);
                 if (e + k < end) {  // wave-uniform
                     const double t = cn_tanh(M, ttab);
+#ifdef LDPC_DIAG_NOMATH
+                    const double En = P * t;
+#else
                     const double En = 2.0 * atanh_f(clip_cl(P / t), ltab);
+#endif
                     if (live) Et[(e + k) * kTile] = En;
                 }
             }
@@ -534,9 +551,9 @@ hipError_t launch_cn(const DevGraph &g, const DevState &st, int it, hipStream_t 
     const unsigned grid = (unsigned)(((st.ntiles + 7) / 8) * 8 * bpt);
     const int par = it & 1;
     if (it == 0)
-        cn_kernel<true><<<grid, 256, 0, s>>>(g, st, bpt, par, g.col_idx, g.row_ptr);
+        cn_kernel<true><<<grid, 256, cn_lds_pad(), s>>>(g, st, bpt, par, g.col_idx, g.row_ptr);
     else
-        cn_kernel<false><<<grid, 256, 0, s>>>(g, st, bpt, par, g.col_idx, g.row_ptr);
+        cn_kernel<false><<<grid, 256, cn_lds_pad(), s>>>(g, st, bpt, par, g.col_idx, g.row_ptr);
     return hipGetLastError();
 }
 

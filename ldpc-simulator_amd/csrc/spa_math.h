@@ -10,12 +10,13 @@
 //          coefficients sit in LDS as {b,c0},{c1,c2},...,{c15,c16} pairs:
 //          9 ds_read_b128 + 16 v_fma_f64 per call.
 // atanh_f  atanh for |q| <= CL (spa_decoder.py:167-168), our design:
-//          |q| < 2^-5: odd Taylor polynomial; else
-//          atanh(a) = (log1p(a) - log1p(-a)) / 2 with each log1p = log(1 +- a)
-//          plus its exact rounding correction, log from a 128-entry
-//          {1/c, -log(1/c)} table and a degree-8 polynomial (glibc-style
-//          reduction r = z/c - 1 by one fma).  About 0.51 ulp; it agrees with
-//          numpy's own arctanh on > 99% of inputs and is faithful on all.
+//          |q| < 2^-5: odd Taylor polynomial; else atanh(a) = log(y)/2 with
+//          y = (1+a)/(1-a) carried as a double-double (faithful quotient +
+//          exact fma residual + the exact rounding errors of 1+a and 1-a), the
+//          log from a 128-entry {1/c, -log(1/c)} table and a degree-8
+//          polynomial (glibc-style reduction r = z/c - 1 by one fma).  About
+//          0.51 ulp; it agrees with numpy's own arctanh on > 98% of inputs and
+//          is faithful on all.
 //          (numpy's arctanh is Intel SVML, which relies on x86-only
 //          reciprocal approximations and cannot be restated portably.)
 #pragma once
@@ -93,11 +94,13 @@ __host__ __device__ __forceinline__ void log_hilo(double x, const LogTab &lt, do
     lo = ((w - hi) + r) + (__builtin_fma(kd, kLn2Lo, t.lo) + r2 * p);
 }
 
-__host__ __device__ __forceinline__ double fast_div(double n, double d) {
+// ~1-ulp reciprocal (v_rcp_f64); only used where the result is corrected or
+// multiplies a tiny correction term.
+__host__ __device__ __forceinline__ double fast_rcp(double d) {
 #if defined(__HIP_DEVICE_COMPILE__)
-    return n * __builtin_amdgcn_rcp(d);  // n is a rounding error: 1-ulp rcp is plenty
+    return __builtin_amdgcn_rcp(d);
 #else
-    return n / d;
+    return 1.0 / d;
 #endif
 }
 
@@ -115,16 +118,21 @@ __host__ __device__ __forceinline__ double atanh_f(double q, const LogTab &lt) {
         p = __builtin_fma(p, a2, 1.0 / 3.0);
         res = __builtin_fma(a * a2, p, a);
     } else {
+        // atanh(a) = log(y)/2, y = (1+a)/(1-a) carried as y_hi + y_lo:
+        // u = 1+a and v = 1-a are rounded, their errors cu, cv exact (u-1, v-1
+        // exact); y_hi = faithful u/v (rcp + one Newton step), its residual
+        // u - y_hi*v exact by fma; y_lo/y_hi ~= (rem + cu - y_hi*cv)/u.
         const double u = 1.0 + a, v = 1.0 - a;
-        const double cu = fast_div(a - (u - 1.0), u);   // exact numerators (u-1, v-1 exact)
-        const double cv = fast_div(-a - (v - 1.0), v);  // 0 for a >= 0.5 (1-a exact)
-        double h1, l1, h2, l2;
-        log_hilo(u, lt, h1, l1);
-        log_hilo(v, lt, h2, l2);
-        const double s = h1 - h2;  // h1 > 0 > h2: no cancellation
-        const double bb = s - h1;
-        const double e = (h1 - (s - bb)) + (-h2 - bb);
-        res = 0.5 * (s + (e + ((l1 - l2) + (cu - cv))));
+        const double cu = a - (u - 1.0);   // exact
+        const double cv = -a - (v - 1.0);  // exact; 0 for a >= 0.5
+        const double rv = fast_rcp(v);
+        const double y0 = u * rv;
+        const double yh = __builtin_fma(__builtin_fma(-y0, v, u), rv, y0);
+        const double rem = __builtin_fma(-yh, v, u);
+        const double corr = __builtin_fma(-yh, cv, rem + cu) * fast_rcp(u);
+        double h, l;
+        log_hilo(yh, lt, h, l);
+        res = 0.5 * (h + (l + corr));
     }
     return dfrom(dbits(res) | (dbits(q) & 0x8000000000000000ull));
 }
