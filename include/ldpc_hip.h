@@ -144,6 +144,26 @@ int ldpc_mc_run(ldpc_decoder *d, uint64_t seed, int32_t n_points, const double *
                 int64_t frames_per_point, int64_t frame0, int32_t max_iter, uint32_t flags,
                 int64_t *counters_out, void *stream);
 
+/* ------------------------------------------------- physical mode (§8 f4)
+ * NOT the reference's arithmetic.  Standard sum-product on a SPARSE graph --
+ * pass H[:, perm] (the ALIST matrix in H_std column order, same code) to
+ * ldpc_graph_create -- with the sign convention made consistent with the tanh
+ * rule (Lambda = -llr), fp32, every frame's state resident in LDS (one
+ * workgroup per frame).  Inputs/outputs keep the reference's conventions:
+ * llr as produced by channel.py, z = (bit estimate) ^ 1, status 0 = OK.
+ * Fails with LDPC_ERANGE when a frame's state does not fit in LDS.
+ */
+int64_t ldpc_phys_lds_bytes(const ldpc_graph *g);
+int ldpc_phys_decode(const ldpc_graph *g, int32_t batch, const double *llr, int32_t max_iter, uint32_t flags,
+                     uint8_t *z_out, int32_t *conv_out, int32_t *status_out, int32_t *iters_out, float *post_out,
+                     void *stream);
+/* On-device frames from d_std (its graph must be the matching H_std = [A|I]:
+ * same generator as ldpc_mc_run), decoded in physical mode on g_phys;
+ * counters as ldpc_mc_run (slot [5] unused). */
+int ldpc_phys_mc_run(ldpc_decoder *d_std, const ldpc_graph *g_phys, uint64_t seed, int32_t n_points,
+                     const double *sigmas, int64_t frames_per_point, int64_t frame0, int32_t max_iter,
+                     uint32_t flags, int64_t *counters_out, void *stream);
+
 /* ------------------------------------------------------------ profiling
  * HIP-event timing of the decoder's own launches, on the stream they are
  * launched on (used by bench.py for the live roofline).  While enabled, every
@@ -155,7 +175,8 @@ int ldpc_mc_run(ldpc_decoder *d, uint64_t seed, int32_t n_points, const double *
 #define LDPC_K_VN 1
 #define LDPC_K_GEN 2
 #define LDPC_K_COUNT 3
-#define LDPC_K_NKINDS 4
+#define LDPC_K_PHYS 4
+#define LDPC_K_NKINDS 5
 int ldpc_profile_enable(ldpc_decoder *d, int enable);
 int ldpc_profile_read(ldpc_decoder *d, double *ms_out, int64_t *launches_out);
 

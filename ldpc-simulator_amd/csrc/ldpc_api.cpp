@@ -44,7 +44,8 @@ struct ldpc_graph {
     int device = 0;
     DevGraph dg{};
     std::vector<int> h_row_ptr, h_col_idx;
-    int *d_ints = nullptr;  // one allocation for all index arrays
+    int *d_ints = nullptr;       // one allocation for all index arrays
+    uint32_t *d_apack = nullptr;  // bit-packed A (std_form graphs only)
 };
 
 struct ldpc_decoder {
@@ -101,6 +102,21 @@ int dev_alloc(T **p, size_t count) {
         return ldpc_fail(LDPC_ENOMEM, "hipMalloc(%zu bytes) failed: %s", count * sizeof(T), hipGetErrorString(e));
     }
     return LDPC_OK;
+}
+
+// Message arrays (E: cap x nnz fp64; T: rare-branch scratch) are only needed by
+// the parity-mode decoder; physical-mode Monte-Carlo never touches them.
+int ensure_messages(ldpc_decoder *d) {
+    if (d->E) return LDPC_OK;
+    const DevGraph &G = d->g->dg;
+    const size_t cap = (size_t)d->cap_tiles * kTile;
+    int rc = dev_alloc(&d->E, cap * (size_t)G.nnz);
+    if (!rc) rc = dev_alloc(&d->T, (size_t)d->nslots * G.max_row_deg * kTile);
+    if (rc) {
+        (void)hipFree(d->E);
+        d->E = nullptr;
+    }
+    return rc;
 }
 
 void state_bind(ldpc_decoder *d, int ntiles, int count) {
@@ -278,8 +294,20 @@ int ldpc_graph_create(int32_t m, int32_t n, const int32_t *row_ptr, const int32_
     if (e == hipSuccess) e = hipMemcpy((void *)G.csc_ptr, csc_ptr.data(), sizeof(int) * (n + 1), hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMemcpy((void *)G.csc_edge, csc_edge.data(), sizeof(int) * nnz, hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMemcpy((void *)G.csc_row, csc_row.data(), sizeof(int) * nnz, hipMemcpyHostToDevice);
+    if (e == hipSuccess && std_form && k > 0) {  // encoder table: A bit-packed per row
+        const size_t kw = (size_t)(k + 31) / 32;
+        std::vector<uint32_t> ap((size_t)m * kw, 0u);
+        for (int r = 0; r < m; ++r)
+            for (int i = row_ptr[r]; i < row_ptr[r + 1]; ++i)
+                if (col_idx[i] < k) ap[(size_t)r * kw + (col_idx[i] >> 5)] |= 1u << (col_idx[i] & 31);
+        if (dev_alloc(&g->d_apack, ap.size())) e = hipErrorOutOfMemory;
+        if (e == hipSuccess)
+            e = hipMemcpy(g->d_apack, ap.data(), sizeof(uint32_t) * ap.size(), hipMemcpyHostToDevice);
+        G.a_packed = g->d_apack;
+    }
     if (e != hipSuccess) {
         (void)hipFree(g->d_ints);
+        (void)hipFree(g->d_apack);
         delete g;
         return ldpc_fail(LDPC_EDEVICE, "ldpc_graph_create: upload failed: %s", hipGetErrorString(e));
     }
@@ -291,6 +319,7 @@ int ldpc_graph_destroy(ldpc_graph *g) {
     if (!g) return LDPC_OK;
     DeviceGuard dg(g->device);
     (void)hipFree(g->d_ints);
+    (void)hipFree(g->d_apack);
     delete g;
     return LDPC_OK;
 }
@@ -325,9 +354,7 @@ int ldpc_decoder_create(const ldpc_graph *g, int32_t max_frames, ldpc_decoder **
     const DevGraph &G = g->dg;
     const size_t kw = (size_t)((G.k + 31) / 32);
     int rc = LDPC_OK;
-    if (!rc) rc = dev_alloc(&d->E, cap * (size_t)G.nnz);
-    d->nslots = scratch_slots();
-    if (!rc) rc = dev_alloc(&d->T, (size_t)d->nslots * G.max_row_deg * kTile);
+    d->nslots = scratch_slots();  // E and T are allocated on first parity-mode use
     if (!rc) rc = dev_alloc(&d->rare, 2 + (size_t)d->cap_tiles * G.m);
     if (!rc && hipMemset(d->rare, 0, sizeof(int) * 2) != hipSuccess)
         rc = ldpc_fail(LDPC_EDEVICE, "ldpc_decoder_create: memset failed");
@@ -388,6 +415,7 @@ int ldpc_decode_f64(ldpc_decoder *d, int32_t batch, const double *llr, int32_t m
     const bool nllr = flags & LDPC_F_NLLR;
     if (dev_ptrs && msg_out) return ldpc_fail(LDPC_EINVAL, "ldpc_decode_f64: msg_out is host-only");
     DeviceGuard dg(d->g->device);
+    if (int rc0 = ensure_messages(d)) return rc0;
     hipStream_t s = (hipStream_t)stream;
     const DevGraph &G = d->g->dg;
     const int n = G.n;
@@ -545,6 +573,7 @@ int ldpc_mc_run(ldpc_decoder *d, uint64_t seed, int32_t n_points, const double *
     for (int p = 0; p < n_points; ++p)
         if (!(sigmas[p] > 0.0)) return ldpc_fail(LDPC_EINVAL, "ldpc_mc_run: sigma[%d] <= 0", p);
     DeviceGuard dg(d->g->device);
+    if (int rc0 = ensure_messages(d)) return rc0;
     hipStream_t s = (hipStream_t)stream;
     const bool nllr = flags & LDPC_F_NLLR;
     const int need = n_points * LDPC_MC_NCOUNT;
@@ -578,6 +607,125 @@ int ldpc_mc_run(ldpc_decoder *d, uint64_t seed, int32_t n_points, const double *
     return LDPC_OK;
 }
 
+// ---------------------------------------------------------- physical mode
+namespace {
+
+constexpr size_t kLdsLimit = 160 * 1024 - 1024;
+
+int phys_grid(const DevGraph &G) {
+    int dev = 0, cus = 256;
+    if (hipGetDevice(&dev) == hipSuccess) {
+        hipDeviceProp_t p;
+        if (hipGetDeviceProperties(&p, dev) == hipSuccess && p.multiProcessorCount > 0) cus = p.multiProcessorCount;
+    }
+    const size_t lds = ldpc::phys_lds_bytes(G) + 64;
+    int per_cu = (int)std::min<size_t>(8, kLdsLimit / lds);  // <= 32 waves / CU at 4 waves per block
+    if (per_cu < 1) per_cu = 1;
+    return cus * per_cu;
+}
+
+int phys_check(const ldpc_graph *g, const char *fn) {
+    if (!g) return ldpc_fail(LDPC_EINVAL, "%s: NULL graph", fn);
+    if (ldpc::phys_lds_bytes(g->dg) > kLdsLimit)
+        return ldpc_fail(LDPC_ERANGE, "%s: %zu bytes of per-frame state exceed LDS", fn, ldpc::phys_lds_bytes(g->dg));
+    return LDPC_OK;
+}
+
+}  // namespace
+
+int64_t ldpc_phys_lds_bytes(const ldpc_graph *g) { return g ? (int64_t)ldpc::phys_lds_bytes(g->dg) : -1; }
+
+int ldpc_phys_decode(const ldpc_graph *g, int32_t batch, const double *llr, int32_t max_iter, uint32_t flags,
+                     uint8_t *z_out, int32_t *conv_out, int32_t *status_out, int32_t *iters_out, float *post_out,
+                     void *stream) {
+    if (int rc = phys_check(g, "ldpc_phys_decode")) return rc;
+    if (batch < 0 || max_iter < 1 || (batch > 0 && !llr))
+        return ldpc_fail(LDPC_EINVAL, "ldpc_phys_decode: bad arguments (batch=%d max_iter=%d)", batch, max_iter);
+    if (batch == 0) return LDPC_OK;
+    DeviceGuard dg(g->device);
+    hipStream_t s = (hipStream_t)stream;
+    const DevGraph &G = g->dg;
+    const size_t n = (size_t)G.n, B = (size_t)batch;
+    if (flags & LDPC_F_DEVICE_PTRS) {
+        HIP_TRY(ldpc::launch_phys(G, llr, 0, batch, max_iter, z_out, conv_out, status_out, iters_out, post_out,
+                                  nullptr, nullptr, std::min(phys_grid(G), batch), s));
+        return LDPC_OK;
+    }
+    double *d_llr = nullptr;
+    uint8_t *d_z = nullptr;
+    int *d_i = nullptr;
+    float *d_post = nullptr;
+    int rc = dev_alloc(&d_llr, B * n);
+    if (!rc) rc = dev_alloc(&d_z, B * n);
+    if (!rc) rc = dev_alloc(&d_i, 3 * B);
+    if (!rc && post_out) rc = dev_alloc(&d_post, B * n);
+    hipError_t e = hipSuccess;
+    if (!rc) {
+        e = hipMemcpyAsync(d_llr, llr, sizeof(double) * B * n, hipMemcpyHostToDevice, s);
+        if (!e) e = ldpc::launch_phys(G, d_llr, 0, batch, max_iter, d_z, d_i, d_i + B, d_i + 2 * B, d_post, nullptr,
+                                     nullptr, std::min(phys_grid(G), batch), s);
+        if (!e && z_out) e = hipMemcpyAsync(z_out, d_z, B * n, hipMemcpyDeviceToHost, s);
+        if (!e && conv_out) e = hipMemcpyAsync(conv_out, d_i, sizeof(int) * B, hipMemcpyDeviceToHost, s);
+        if (!e && status_out) e = hipMemcpyAsync(status_out, d_i + B, sizeof(int) * B, hipMemcpyDeviceToHost, s);
+        if (!e && iters_out) e = hipMemcpyAsync(iters_out, d_i + 2 * B, sizeof(int) * B, hipMemcpyDeviceToHost, s);
+        if (!e && post_out) e = hipMemcpyAsync(post_out, d_post, sizeof(float) * B * n, hipMemcpyDeviceToHost, s);
+        if (!e) e = hipStreamSynchronize(s);
+        if (e) rc = ldpc_fail(LDPC_EDEVICE, "ldpc_phys_decode: %s", hipGetErrorString(e));
+    }
+    (void)hipFree(d_llr);
+    (void)hipFree(d_z);
+    (void)hipFree(d_i);
+    (void)hipFree(d_post);
+    return rc;
+}
+
+int ldpc_phys_mc_run(ldpc_decoder *d, const ldpc_graph *gp, uint64_t seed, int32_t n_points, const double *sigmas,
+                     int64_t frames_per_point, int64_t frame0, int32_t max_iter, uint32_t flags, int64_t *counters_out,
+                     void *stream) {
+    if (int rc = phys_check(gp, "ldpc_phys_mc_run")) return rc;
+    if (!d || n_points <= 0 || !sigmas || frames_per_point < 0 || frame0 < 0 || max_iter < 1 || !counters_out)
+        return ldpc_fail(LDPC_EINVAL, "ldpc_phys_mc_run: bad arguments");
+    const DevGraph &G = d->g->dg;
+    const DevGraph &P = gp->dg;
+    if (!G.std_form) return ldpc_fail(LDPC_EINVAL, "ldpc_phys_mc_run: d_std graph is not [A | I_m]");
+    if (P.n != G.n || P.k != G.k)
+        return ldpc_fail(LDPC_EINVAL, "ldpc_phys_mc_run: physical graph shape %dx%d != %dx%d", P.m, P.n, G.m, G.n);
+    for (int p = 0; p < n_points; ++p)
+        if (!(sigmas[p] > 0.0)) return ldpc_fail(LDPC_EINVAL, "ldpc_phys_mc_run: sigma[%d] <= 0", p);
+    (void)flags;
+    DeviceGuard dg(d->g->device);
+    hipStream_t s = (hipStream_t)stream;
+    const int need = n_points * LDPC_MC_NCOUNT;
+    if (d->counters_cap < need) {
+        (void)hipFree(d->counters);
+        d->counters = nullptr;
+        d->counters_cap = 0;
+        if (int rc = dev_alloc(&d->counters, (size_t)need)) return rc;
+        d->counters_cap = need;
+    }
+    HIP_TRY(hipMemsetAsync(d->counters, 0, sizeof(unsigned long long) * need, s));
+    const int64_t cap = (int64_t)d->cap_tiles * kTile;
+    for (int p = 0; p < n_points; ++p) {
+        for (int64_t start = 0; start < frames_per_point; start += cap) {
+            const int cnt = (int)std::min<int64_t>(cap, frames_per_point - start);
+            state_bind(d, (cnt + kTile - 1) / kTile, cnt);
+            const DevState st = d->st;
+            HIP_TRY(timed(d, LDPC_K_GEN, s,
+                          [&] { return ldpc::launch_generate(G, st, seed, p, sigmas[p], frame0 + start, s); }));
+            HIP_TRY(timed(d, LDPC_K_PHYS, s, [&] {
+                return ldpc::launch_phys(P, st.ch, 1, cnt, max_iter, nullptr, nullptr, nullptr, nullptr, nullptr,
+                                         st.ubits, d->counters + (size_t)p * LDPC_MC_NCOUNT,
+                                         std::min(phys_grid(P), cnt), s);
+            }));
+        }
+    }
+    std::vector<unsigned long long> h(need);
+    HIP_TRY(hipMemcpyAsync(h.data(), d->counters, sizeof(unsigned long long) * need, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    for (int i = 0; i < need; ++i) counters_out[i] = (int64_t)h[i];
+    return LDPC_OK;
+}
+
 // -------------------------------------------------------------- profiling
 int ldpc_profile_enable(ldpc_decoder *d, int enable) {
     if (!d) return ldpc_fail(LDPC_EINVAL, "ldpc_profile_enable: NULL decoder");
@@ -588,8 +736,8 @@ int ldpc_profile_enable(ldpc_decoder *d, int enable) {
 int ldpc_profile_read(ldpc_decoder *d, double *ms_out, int64_t *launches_out) {
     if (!d) return ldpc_fail(LDPC_EINVAL, "ldpc_profile_read: NULL decoder");
     DeviceGuard dg(d->g->device);
-    double ms[LDPC_K_NKINDS] = {0, 0, 0, 0};
-    int64_t cnt[LDPC_K_NKINDS] = {0, 0, 0, 0};
+    double ms[LDPC_K_NKINDS] = {};
+    int64_t cnt[LDPC_K_NKINDS] = {};
     for (auto &sp : d->spans) {
         HIP_TRY(hipEventSynchronize(sp.b));
         float t = 0.f;

@@ -29,6 +29,7 @@ struct DevGraph {
     const int *csc_ptr;      // [n+1]
     const int *csc_edge;     // [nnz] CSR edge id, rows ascending within a column
     const int *csc_row;      // [nnz] row of that edge
+    const uint32_t *a_packed;  // [m][kw] bit j of row r = A[r][j] (encoder; std_form only)
 };
 
 struct DevState {
@@ -60,6 +61,12 @@ hipError_t launch_export_frames(const DevGraph &g, const DevState &st, uint8_t *
                                 hipStream_t s);
 hipError_t launch_count(const DevGraph &g, const DevState &st, unsigned long long *counters,
                         hipStream_t s);
+
+// physical mode (phys_kernels.hip)
+size_t phys_lds_bytes(const DevGraph &g);
+hipError_t launch_phys(const DevGraph &g, const double *llr, int layout, int count, int max_iter, uint8_t *z,
+                       int *conv, int *status, int *iters, float *post, const uint32_t *ubits,
+                       unsigned long long *ctr, int grid, hipStream_t s);
 
 // --- Philox4x32-10 (Salmon et al., SC'11), shared by host tests and device ---
 __host__ __device__ inline void philox4x32_10(uint32_t c[4], uint32_t k0, uint32_t k1) {

@@ -415,7 +415,8 @@ __device__ __forceinline__ double u52(uint32_t hi, uint32_t lo) {
 }
 
 __global__ __launch_bounds__(64) void generate_kernel(DevGraph g, DevState st, uint64_t seed, int snr_point,
-                                                      double sigma, int64_t frame0) {
+                                                      double sigma, int64_t frame0,
+                                                      const uint32_t *__restrict__ apack) {
     extern __shared__ uint32_t ul[];
     const int tile = blockIdx.x;
     const int lane = threadIdx.x;
@@ -456,13 +457,11 @@ __global__ __launch_bounds__(64) void generate_kernel(DevGraph g, DevState st, u
             uint32_t bit;
             if (j < g.k) {
                 bit = (ul[(j >> 5) * kTile + lane] >> (j & 31)) & 1u;
-            } else {  // parity bit of row j-k: XOR of u over A's columns of that row
-                const int rr = j - g.k;
-                bit = 0u;
-                for (int e = g.row_ptr[rr]; e < g.row_ptr[rr + 1]; ++e) {
-                    const int cc = g.col_idx[e];
-                    if (cc < g.k) bit ^= (ul[(cc >> 5) * kTile + lane] >> (cc & 31)) & 1u;
-                }
+            } else {  // parity bit of row j-k = parity(A_row & u), A bit-packed (uniform loads)
+                const uint32_t *ar = apack + (size_t)(j - g.k) * kw;
+                uint32_t acc = 0u;
+                for (int w = 0; w < kw; ++w) acc ^= ar[w] & ul[w * kTile + lane];
+                bit = (uint32_t)__popc(acc) & 1u;
             }
             const double x = bit ? 1.0 : -1.0;
             const double y = x + s2 * gz[q];
@@ -594,7 +593,7 @@ hipError_t launch_export_msgs(const DevGraph &g, const DevState &st, double *out
 hipError_t launch_generate(const DevGraph &g, const DevState &st, uint64_t seed, int snr_point, double sigma,
                            int64_t frame0, hipStream_t s) {
     const size_t lds = (size_t)((g.k + 31) >> 5) * kTile * sizeof(uint32_t);
-    generate_kernel<<<st.ntiles, kTile, lds, s>>>(g, st, seed, snr_point, sigma, frame0);
+    generate_kernel<<<st.ntiles, kTile, lds, s>>>(g, st, seed, snr_point, sigma, frame0, g.a_packed);
     return hipGetLastError();
 }
 

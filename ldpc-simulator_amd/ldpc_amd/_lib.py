@@ -25,6 +25,7 @@ EXPORTED = (
     "ldpc_decoder_bytes", "ldpc_decoder_create", "ldpc_decoder_destroy", "ldpc_decoder_capacity",
     "ldpc_decode_f64", "ldpc_generate_frames", "ldpc_mc_run",
     "ldpc_profile_enable", "ldpc_profile_read",
+    "ldpc_phys_lds_bytes", "ldpc_phys_decode", "ldpc_phys_mc_run",
 )
 
 
@@ -67,6 +68,10 @@ def _declare(lib):
         "ldpc_mc_run": (ctypes.c_int, [c_vp, c_u64, c_i32, P(c_dbl), c_i64, c_i64, c_i32, c_u32,
                                        P(c_i64), c_vp]),
         "ldpc_profile_enable": (ctypes.c_int, [c_vp, ctypes.c_int]),
+        "ldpc_phys_lds_bytes": (c_i64, [c_vp]),
+        "ldpc_phys_decode": (ctypes.c_int, [c_vp, c_i32, c_vp, c_i32, c_u32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
+        "ldpc_phys_mc_run": (ctypes.c_int, [c_vp, c_vp, c_u64, c_i32, P(c_dbl), c_i64, c_i64, c_i32, c_u32,
+                                            P(c_i64), c_vp]),
         "ldpc_profile_read": (ctypes.c_int, [c_vp, P(c_dbl), P(c_i64)]),
     }
     for name, (res, args) in sig.items():

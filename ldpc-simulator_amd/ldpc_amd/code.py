@@ -83,6 +83,13 @@ class EncoderDecoderData:
                                            A]).tocsr().astype(np.int32)
         self._decoder_structures_initialized = False
 
+    def physical_matrix(self):
+        """H[:, perm]: the sparse ALIST graph in H_std's column order (same code;
+        row operations do not change the null space) -- physical mode, §8 f4."""
+        Hp = sparse.csr_matrix(self._h)[:, self._permutation].tocsr()
+        Hp.sort_indices()
+        return Hp
+
     # reference-compatible accessors
     def get_decoder_structures(self):
         coo = self._h_std.tocoo()

@@ -64,6 +64,23 @@ class Graph:
             self._h = None
 
 
+def phys_decode(graph, llr, max_iter, post=False):
+    """Physical-mode decode of [B, n] LLRs on a sparse graph (H[:, perm])."""
+    llr = np.ascontiguousarray(np.atleast_2d(np.asarray(llr, dtype=np.float64)))
+    B, n = llr.shape
+    if n != graph.n:
+        raise ValueError(f"llr must be [batch, {graph.n}]")
+    z = np.empty((B, n), np.uint8)
+    conv = np.empty(B, np.int32)
+    status = np.empty(B, np.int32)
+    iters = np.empty(B, np.int32)
+    Lp = np.empty((B, n), np.float32) if post else None
+    check("ldpc_phys_decode", _lib.lib().ldpc_phys_decode(
+        graph.handle, B, _lib.ptr(llr), int(max_iter), 0, _lib.ptr(z), _lib.ptr(conv), _lib.ptr(status),
+        _lib.ptr(iters), _lib.ptr(Lp), None))
+    return DecodeResult(z=z, conv=conv, status=status, iters=iters, post=Lp)
+
+
 class DecodeResult(dict):
     __getattr__ = dict.__getitem__
 
@@ -126,15 +143,25 @@ class Decoder:
             out.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)), None))
         return out
 
-    KINDS = ("cn", "vn", "generate", "count")
+    def phys_mc_run(self, phys_graph, seed, sigmas, frames_per_point, frame0, max_iter):
+        """Physical mode (§8 f4): same on-device frames, decoded on the sparse graph."""
+        sig = np.ascontiguousarray(np.asarray(sigmas, dtype=np.float64))
+        out = np.zeros((len(sig), LDPC_MC_NCOUNT), np.int64)
+        check("ldpc_phys_mc_run", _lib.lib().ldpc_phys_mc_run(
+            self._h, phys_graph.handle, int(seed), len(sig), sig.ctypes.data_as(ctypes.POINTER(ctypes.c_double)),
+            int(frames_per_point), int(frame0), int(max_iter), 0,
+            out.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)), None))
+        return out
+
+    KINDS = ("cn", "vn", "generate", "count", "phys")
 
     def profile(self, enable=True):
         check("ldpc_profile_enable", _lib.lib().ldpc_profile_enable(self._h, 1 if enable else 0))
 
     def profile_read(self):
         """{kind: (total_ms, launches)} of this decoder's launches since the last read."""
-        ms = (ctypes.c_double * 4)()
-        n = (ctypes.c_int64 * 4)()
+        ms = (ctypes.c_double * len(self.KINDS))()
+        n = (ctypes.c_int64 * len(self.KINDS))()
         check("ldpc_profile_read", _lib.lib().ldpc_profile_read(self._h, ms, n))
         return {k: (ms[i], n[i]) for i, k in enumerate(self.KINDS)}
 

@@ -41,6 +41,8 @@ def lib():
         L.oracle_philox4x32_10.restype = None
         L.oracle_philox4x32_10.argtypes = [vp, ctypes.c_uint32, ctypes.c_uint32]
         L.oracle_max_threads.restype = ctypes.c_int
+        L.oracle_phys_decode.restype = ctypes.c_int
+        L.oracle_phys_decode.argtypes = [i32, i32, vp, vp, i32, vp, i32, vp, vp, vp, vp]
         L.oracle_np_tanh.restype = dbl
         L.oracle_np_tanh.argtypes = [dbl]
         L.oracle_set_tanh_nudge.restype = None
@@ -94,6 +96,21 @@ def conditioning_slack(H_std, llr, max_iter, nllr=False, factor=4.0):
     finally:
         lib().oracle_set_tanh_nudge(0)
     return factor * np.abs(pert["post"] - base["post"]), factor * np.abs(pert["msgs"] - base["msgs"])
+
+
+def phys_decode(H_phys, llr, max_iter):
+    """CPU restatement of the physical mode (our design, oracle/phys_oracle.c)."""
+    m, n, indptr, indices = _csr(H_phys)
+    llr = np.ascontiguousarray(np.atleast_2d(np.asarray(llr, dtype=np.float64)))
+    B = llr.shape[0]
+    z = np.empty((B, n), np.uint8)
+    conv = np.empty(B, np.int32)
+    iters = np.empty(B, np.int32)
+    post = np.empty((B, n), np.float32)
+    if lib().oracle_phys_decode(m, n, _p(indptr), _p(indices), B, _p(llr), int(max_iter),
+                                _p(z), _p(conv), _p(iters), _p(post)) != 0:
+        raise ValueError("oracle_phys_decode rejected its arguments")
+    return dict(z=z, conv=conv, status=(conv < 0).astype(np.int32), iters=iters, post=post)
 
 
 def np_tanh(x):
