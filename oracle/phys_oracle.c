@@ -13,9 +13,12 @@
 #include <stdlib.h>
 #include <string.h>
 
+/* same formula as the GPU's default (hardware exp/log) path */
 static float phi(float x) {
     x = fminf(fmaxf(x, 1.0e-7f), 30.0f);
-    return log1pf(2.0f / expm1f(x));
+    if (x < 0.03125f) return logf(2.0f * (1.0f / x)) + x * x * (1.0f / 12.0f);
+    const float t = expf(x);
+    return logf((t + 1.0f) * (1.0f / (t - 1.0f)));
 }
 
 int oracle_phys_decode(int m, int n, const int *row_ptr, const int *col_idx, int batch, const double *llr,
