@@ -41,7 +41,10 @@ def parse():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--code", default="wimax_576_0.5")
     ap.add_argument("--frames", type=int, default=65536, help="frames per GPU per step")
-    ap.add_argument("--chunk", type=int, default=0, help="decoder chunk (frames); 0 = whole batch")
+    ap.add_argument("--chunk", type=int, default=0, help="decoder slots (frames resident at once); 0 = whole batch")
+    ap.add_argument("--schedule", choices=("stream", "static"), default="stream",
+                    help="stream: a slot takes the next frame as soon as its frame stops; static: chunks decoded "
+                         "to completion (same frames, same counters)")
     ap.add_argument("--iters", type=int, default=50)
     ap.add_argument("--snr", type=float, default=0.0, help="reference SNR axis (dB), speed=1")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU-baseline sample budget (0 = skip)")
@@ -170,7 +173,7 @@ def main():
         if pgraph is not None:
             c = dec.phys_mc_run(pgraph, SEED, [sigma], B, frame0, args.iters)
         else:
-            c = dec.mc_run(SEED, [sigma], B, frame0, args.iters)
+            c = dec.mc_run(SEED, [sigma], B, frame0, args.iters, static=args.schedule == "static")
         if record:
             local_totals[:] += c
         return allreduce_counters(dist, c, local)
@@ -232,7 +235,7 @@ def main():
                         f"(reference axis, speed 1), {B} frames/GPU/step",
             "code": args.code, "n": n, "k": k, "edges_H_std": nnz, "max_iter": args.iters,
             "snr_db": args.snr, "frames_per_gpu": B, "global_batch": B * world,
-            "parallelism": f"frame-sharded x{world}", "chunk_frames": chunk,
+            "parallelism": f"frame-sharded x{world}", "chunk_frames": chunk, "schedule": args.schedule,
         },
         "fer": totals[0, 1] / frames_total,
         "ber": totals[0, 2] / (k * frames_total),

@@ -43,6 +43,7 @@ extern "C" {
 /* decode flags */
 #define LDPC_F_NLLR 0x1u        /* normalized-LLR metric, spa_decoder.py:210-228  */
 #define LDPC_F_DEVICE_PTRS 0x2u /* I/O pointers are device pointers, async        */
+#define LDPC_F_STATIC 0x4u      /* ldpc_mc_run: chunked schedule, no slot refill  */
 
 typedef struct ldpc_hstd ldpc_hstd;       /* standard-form parity-check matrix  */
 typedef struct ldpc_graph ldpc_graph;     /* H_std uploaded to one GPU          */
@@ -138,6 +139,11 @@ int ldpc_generate_frames(ldpc_decoder *d, uint64_t seed, int32_t snr_point, doub
  *   [3] sum of convergence_iteration over converged frames  [4] converged frames
  *   [5] sum over frames of the final normalized-LLR count (nllr = count/k)
  *   [6] iterations executed (for roofline byte accounting)
+ * Schedule: by default the decoder's max_frames are slots that are refilled
+ * with the next frame index as soon as their frame stops (syndrome zero or
+ * max_iter), so throughput follows the average iteration count rather than
+ * the slowest frame of a tile; LDPC_F_STATIC decodes chunks of max_frames to
+ * completion instead.  Both decode the same frames: counters are identical.
  */
 #define LDPC_MC_NCOUNT 7
 int ldpc_mc_run(ldpc_decoder *d, uint64_t seed, int32_t n_points, const double *sigmas,

@@ -54,12 +54,12 @@ struct ldpc_decoder {
     double *E = nullptr, *T = nullptr, *L = nullptr, *ch = nullptr;
     int *rare = nullptr;  // rare_count[2] + rare_list[cap_tiles*m]
     int nslots = 0;
-    int *ints = nullptr;  // done, conv, status, iters, nllr_cnt (cap frames each) + tile_active
+    int *ints = nullptr;  // done, conv, status, iters, nllr_cnt, fresh, refill (cap frames each) + tile_active
     uint32_t *ubits = nullptr;
     // staging for host I/O
     double *llr_stage = nullptr, *post_stage = nullptr;
     uint8_t *z_stage = nullptr;
-    unsigned long long *counters = nullptr;
+    unsigned long long *counters = nullptr;  // [counters_cap] + 1 frame-index counter (streaming)
     int counters_cap = 0;
     DevState st{};
     // profiling (ldpc_profile_*)
@@ -134,7 +134,9 @@ void state_bind(ldpc_decoder *d, int ntiles, int count) {
     s.status = d->ints + 2 * cap;
     s.iters = d->ints + 3 * cap;
     s.nllr_cnt = d->ints + 4 * cap;
-    s.tile_active = d->ints + 5 * cap;
+    s.fresh = d->ints + 5 * cap;
+    s.refill = d->ints + 6 * cap;
+    s.tile_active = d->ints + 7 * cap;
     s.ubits = d->ubits;
     s.nllr_hist = nullptr;
     s.hist_stride = 0;
@@ -188,7 +190,7 @@ size_t workspace_bytes(const DevGraph &g, int cap_tiles) {
     b += (size_t)scratch_slots() * g.max_row_deg * kTile * 8;            // T pool
     b += 4 * (2 + (size_t)cap_tiles * g.m);                               // rare list
     b += 2 * cap * (size_t)g.n * 8;    // L, ch
-    b += (5 * cap + cap_tiles) * 4;    // per-frame ints + tile flags
+    b += (7 * cap + cap_tiles) * 4;    // per-frame ints + tile flags
     b += cap * kw * 4;                 // ubits
     b += 2 * cap * (size_t)g.n * 8;    // llr/post staging
     b += cap * (size_t)g.n;            // z staging
@@ -360,7 +362,7 @@ int ldpc_decoder_create(const ldpc_graph *g, int32_t max_frames, ldpc_decoder **
         rc = ldpc_fail(LDPC_EDEVICE, "ldpc_decoder_create: memset failed");
     if (!rc) rc = dev_alloc(&d->L, cap * (size_t)G.n);
     if (!rc) rc = dev_alloc(&d->ch, cap * (size_t)G.n);
-    if (!rc) rc = dev_alloc(&d->ints, 5 * cap + (size_t)d->cap_tiles);
+    if (!rc) rc = dev_alloc(&d->ints, 7 * cap + (size_t)d->cap_tiles);
     if (!rc) rc = dev_alloc(&d->ubits, std::max<size_t>(cap * kw, 1));
     if (!rc) rc = dev_alloc(&d->llr_stage, cap * (size_t)G.n);
     if (!rc) rc = dev_alloc(&d->post_stage, cap * (size_t)G.n);
@@ -564,6 +566,55 @@ int ldpc_generate_frames(ldpc_decoder *d, uint64_t seed, int32_t snr_point, doub
     return LDPC_OK;
 }
 
+namespace {
+
+// Streaming schedule of one SNR point: the decoder's cap frames are slots.  A
+// slot whose frame finishes (vn_kernel) is refilled with the next frame index
+// (refill_kernel), so no slot waits for the slowest frame of its tile or
+// chunk; only the last frames of the point form a tail.  Frames, and the
+// counters summed over them, are exactly the static schedule's.
+int mc_stream_point(ldpc_decoder *d, uint64_t seed, int p, double sigma, int64_t total, int64_t frame0, int max_iter,
+                    bool nllr, hipStream_t s) {
+    if (total == 0) return LDPC_OK;
+    const DevGraph &G = d->g->dg;
+    const int ntiles = (int)std::min<int64_t>(d->cap_tiles, (total + kTile - 1) / kTile);
+    state_bind(d, ntiles, ntiles * kTile);
+    const DevState st = d->st;
+    unsigned long long *ctr = d->counters + (size_t)p * LDPC_MC_NCOUNT;
+    unsigned long long *next = d->counters + d->counters_cap;
+    HIP_TRY(ldpc::launch_stream_init(G, st, s));
+    HIP_TRY(hipMemsetAsync(next, 0, sizeof(unsigned long long), s));
+    auto refill = [&] {
+        return timed(d, LDPC_K_GEN, s,
+                     [&] { return ldpc::launch_refill(G, st, seed, p, sigma, frame0, total, next, s); });
+    };
+    HIP_TRY(refill());
+    const int64_t slots = (int64_t)ntiles * kTile;
+    const int64_t min_steps = (total + slots - 1) / slots;            // every slot needs >= 1 step per frame
+    const int64_t max_steps = (min_steps + 1) * (int64_t)max_iter;   // every frame stops by max_iter
+    constexpr int kPoll = 4;
+    int64_t step = 0;
+    for (;;) {
+        const int64_t until = std::max<int64_t>(step + kPoll, min_steps);
+        for (; step < until; ++step) {
+            const int par = (int)(step & 1);
+            HIP_TRY(timed(d, LDPC_K_CN, s, [&] { return ldpc::launch_cn(G, st, par, s, true); }));
+            HIP_TRY(ldpc::launch_cn_rare(G, st, par, s, true));
+            HIP_TRY(timed(d, LDPC_K_VN, s, [&] { return ldpc::launch_vn(G, st, 0, max_iter, nllr, s, ctr); }));
+            HIP_TRY(refill());
+        }
+        unsigned long long finished = 0;
+        HIP_TRY(hipMemcpyAsync(&finished, ctr, sizeof(finished), hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipStreamSynchronize(s));
+        if ((int64_t)finished >= total) return LDPC_OK;
+        if (step > max_steps)
+            return ldpc_fail(LDPC_EDEVICE, "ldpc_mc_run: streaming schedule did not drain (%llu of %lld frames)",
+                             finished, (long long)total);
+    }
+}
+
+}  // namespace
+
 int ldpc_mc_run(ldpc_decoder *d, uint64_t seed, int32_t n_points, const double *sigmas, int64_t frames_per_point,
                 int64_t frame0, int32_t max_iter, uint32_t flags, int64_t *counters_out, void *stream) {
     if (!d || n_points <= 0 || !sigmas || frames_per_point < 0 || frame0 < 0 || max_iter < 1 || !counters_out)
@@ -581,11 +632,15 @@ int ldpc_mc_run(ldpc_decoder *d, uint64_t seed, int32_t n_points, const double *
         (void)hipFree(d->counters);
         d->counters = nullptr;
         d->counters_cap = 0;
-        if (int rc = dev_alloc(&d->counters, (size_t)need)) return rc;
+        if (int rc = dev_alloc(&d->counters, (size_t)need + 1)) return rc;
         d->counters_cap = need;
     }
     HIP_TRY(hipMemsetAsync(d->counters, 0, sizeof(unsigned long long) * need, s));
     const int64_t cap = (int64_t)d->cap_tiles * kTile;
+    if (!(flags & LDPC_F_STATIC)) {
+        for (int p = 0; p < n_points; ++p)
+            if (int rc = mc_stream_point(d, seed, p, sigmas[p], frames_per_point, frame0, max_iter, nllr, s)) return rc;
+    } else
     for (int p = 0; p < n_points; ++p) {
         for (int64_t start = 0; start < frames_per_point; start += cap) {
             const int cnt = (int)std::min<int64_t>(cap, frames_per_point - start);
@@ -700,7 +755,7 @@ int ldpc_phys_mc_run(ldpc_decoder *d, const ldpc_graph *gp, uint64_t seed, int32
         (void)hipFree(d->counters);
         d->counters = nullptr;
         d->counters_cap = 0;
-        if (int rc = dev_alloc(&d->counters, (size_t)need)) return rc;
+        if (int rc = dev_alloc(&d->counters, (size_t)need + 1)) return rc;
         d->counters_cap = need;
     }
     HIP_TRY(hipMemsetAsync(d->counters, 0, sizeof(unsigned long long) * need, s));

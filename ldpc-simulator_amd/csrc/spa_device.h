@@ -11,7 +11,8 @@
 //   L   [tile][n][64]    fp64 a-posteriori LLRs
 //   ch  [tile][n][64]    fp64 channel LLRs
 //   ub  [tile][kw][64]   info bits (Monte-Carlo path), kw = ceil(k/32)
-// Per frame: done / conv / status / iters / nllr count; per tile: active flag.
+// Per frame: done / conv / status / iters / nllr count (+ fresh / refill of the
+// streaming Monte-Carlo schedule); per tile: active flag.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <cstdint>
@@ -36,6 +37,7 @@ struct DevState {
     double *E, *T, *L, *ch;
     int *done, *conv, *status, *iters, *nllr_cnt;
     int *tile_active;
+    int *fresh, *refill;     // streaming Monte-Carlo: lane holds a new frame / lane wants one
     int *rare_list;          // [ntiles*m] tile*m+row of rows left to cn_rare_kernel
     int *rare_count;         // [2] per iteration parity
     int nslots;
@@ -49,9 +51,15 @@ struct DevState {
 // --- launchers (spa_kernels.hip); all asynchronous on `s` ---
 hipError_t launch_reset(const DevGraph &g, const DevState &st, hipStream_t s);
 hipError_t launch_load_llr(const DevGraph &g, const DevState &st, const double *llr, hipStream_t s);
-hipError_t launch_cn(const DevGraph &g, const DevState &st, int it, hipStream_t s);
-hipError_t launch_cn_rare(const DevGraph &g, const DevState &st, int it, hipStream_t s);
-hipError_t launch_vn(const DevGraph &g, const DevState &st, int it, int max_iter, bool nllr, hipStream_t s);
+// stream = the streaming Monte-Carlo schedule (lanes at different iterations,
+// see refill_kernel); stream_ctr != null selects the streaming VN.
+hipError_t launch_cn(const DevGraph &g, const DevState &st, int it, hipStream_t s, bool stream = false);
+hipError_t launch_cn_rare(const DevGraph &g, const DevState &st, int it, hipStream_t s, bool stream = false);
+hipError_t launch_vn(const DevGraph &g, const DevState &st, int it, int max_iter, bool nllr, hipStream_t s,
+                     unsigned long long *stream_ctr = nullptr);
+hipError_t launch_stream_init(const DevGraph &g, const DevState &st, hipStream_t s);
+hipError_t launch_refill(const DevGraph &g, const DevState &st, uint64_t seed, int snr_point, double sigma,
+                         int64_t frame0, int64_t total, unsigned long long *next, hipStream_t s);
 hipError_t launch_finalize(const DevGraph &g, const DevState &st, uint8_t *z, double *post,
                            hipStream_t s);
 hipError_t launch_export_msgs(const DevGraph &g, const DevState &st, double *out, hipStream_t s);

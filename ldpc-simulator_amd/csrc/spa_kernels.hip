@@ -116,15 +116,19 @@ constexpr int kPf = LDPC_PF;  // edges in flight per wavefront (software pipelin
 
 // Register ring of the next kPf edges' (L[col], E_old) loads.  take(k, e)
 // returns M for edge e (ring slot k) and issues the loads for edge e + kPf.
-template <bool kFirst>
+// kStream (streaming Monte-Carlo): a lane whose frame was just loaded
+// ("fresh", L = ch) takes M = L - 0 -- its iteration 0 -- while the other
+// lanes of the wavefront take M = L - E_old.
+template <bool kFirst, bool kStream>
 struct EdgeStream {
     const int *__restrict__ col;
     const double *Lt, *Et;
     int end;
+    bool fresh;
     double lv[kPf], eo[kPf];
     __device__ __forceinline__ EdgeStream(const int *__restrict__ col_, const double *L_, const double *E_, int beg,
-                                          int end_)
-        : col(col_), Lt(L_), Et(E_), end(end_) {
+                                          int end_, bool fresh_)
+        : col(col_), Lt(L_), Et(E_), end(end_), fresh(fresh_) {
 #pragma unroll
         for (int k = 0; k < kPf; ++k) fetch(k, beg + k);
     }
@@ -136,12 +140,12 @@ struct EdgeStream {
         eo[k] = kFirst ? 0.0 : Et[i * kTile];
     }
     __device__ __forceinline__ double take(int k, int e) {
-        const double M = kFirst ? lv[k] : lv[k] - eo[k];
+        const double M = kFirst ? lv[k] : lv[k] - ((kStream && fresh) ? 0.0 : eo[k]);
         fetch(k, e + kPf);
         return M;
     }
 };
-template <bool kFirst>
+template <bool kFirst, bool kStream>
 __global__ __launch_bounds__(256, LDPC_CN_WAVES) void cn_kernel(DevGraph g, DevState st, int blocks_per_tile,
                                                                 int it_parity, const int *__restrict__ col_idx,
                                                                 const int *__restrict__ row_ptr) {
@@ -166,6 +170,7 @@ __global__ __launch_bounds__(256, LDPC_CN_WAVES) void cn_kernel(DevGraph g, DevS
 
     const int f = tile * kTile + lane;
     const bool live = st.done[f] == 0;
+    const bool fresh = kStream && st.fresh[f] != 0;
     double *Et = st.E + (size_t)tile * g.nnz * kTile + lane;
     const double *Lt = (kFirst ? st.ch : st.L) + (size_t)tile * g.n * kTile + lane;
 
@@ -175,7 +180,7 @@ __global__ __launch_bounds__(256, LDPC_CN_WAVES) void cn_kernel(DevGraph g, DevS
     double P = 1.0;
     bool tiny = false;
     {
-        EdgeStream<kFirst> es(col_idx, Lt, Et, beg, end);
+        EdgeStream<kFirst, kStream> es(col_idx, Lt, Et, beg, end, fresh);
         for (int e = beg; e < end; e += kPf) {
 #pragma unroll
             for (int k = 0; k < kPf; ++k) {
@@ -192,7 +197,7 @@ __global__ __launch_bounds__(256, LDPC_CN_WAVES) void cn_kernel(DevGraph g, DevS
         // pass 2: recompute t from the same E_old / L bits (identical result),
         // E_new = 2 atanh(clip(P/t)) written over E_old.  24 B of HBM per edge
         // instead of parking t (32 B).
-        EdgeStream<kFirst> es(col_idx, Lt, Et, beg, end);
+        EdgeStream<kFirst, kStream> es(col_idx, Lt, Et, beg, end, fresh);
         for (int e = beg; e < end; e += kPf) {
 #pragma unroll
             for (int k = 0; k < kPf; ++k) {
@@ -221,7 +226,7 @@ __global__ __launch_bounds__(256, LDPC_CN_WAVES) void cn_kernel(DevGraph g, DevS
 
 // Rows recorded by cn_kernel: same update, with t parked in this wavefront's
 // own scratch slot (slot = global wavefront id; grid-stride over the list).
-template <bool kFirst>
+template <bool kFirst, bool kStream>
 __global__ __launch_bounds__(256) void cn_rare_kernel(DevGraph g, DevState st, int it_parity) {
     __shared__ MathLds mlds;
     const int count = st.rare_count[it_parity];
@@ -241,12 +246,13 @@ __global__ __launch_bounds__(256) void cn_rare_kernel(DevGraph g, DevState st, i
         const int beg = g.row_ptr[row], end = g.row_ptr[row + 1];
         const int f = tile * kTile + lane;
         const bool live = st.done[f] == 0;
+        const bool fresh = kStream && st.fresh[f] != 0;
         double *Et = st.E + (size_t)tile * g.nnz * kTile + lane;
         const double *Lt = (kFirst ? st.ch : st.L) + (size_t)tile * g.n * kTile + lane;
         double P = 1.0;
         for (int e = beg; e < end; ++e) {
             double M = Lt[g.col_idx[e] * kTile];
-            if (!kFirst) M = M - Et[e * kTile];
+            if (!kFirst) M = M - (fresh ? 0.0 : Et[e * kTile]);
             const double t = cn_tanh(M, ttab);
             P = (e == beg) ? t : P * t;
             Tt[(e - beg) * kTile] = t;
@@ -273,18 +279,33 @@ __global__ __launch_bounds__(256) void cn_rare_kernel(DevGraph g, DevState st, i
 }
 
 // ------------------------------------------------------- VN + syndrome pass
-template <bool kFirst>
+__device__ __forceinline__ unsigned long long wave_sum(unsigned long long v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    return v;
+}
+
+
+// kStream (streaming Monte-Carlo): every lane is at its own iteration
+// (iters[f] = iterations its frame has completed); `last` is max_iter.  A
+// frame that finishes here adds its counters (count_kernel's definitions) to
+// ctr and flags its lane for refill_kernel.
+template <bool kFirst, bool kStream>
 __global__ __launch_bounds__(1024) void vn_kernel(DevGraph g, DevState st, int it, int last, int nllr,
                                                   const int *__restrict__ csc_ptr,
                                                   const int *__restrict__ csc_edge,
-                                                  const int *__restrict__ csc_row) {
+                                                  const int *__restrict__ csc_row, unsigned long long *ctr) {
     extern __shared__ uint32_t par[];  // [mw][64] row parities of z^1, one column per frame
     __shared__ int cnt_lds[kTile];
+    __shared__ int err_lds[kTile];
     const int tile = blockIdx.x;
     if (!st.tile_active[tile]) return;
     const int mw = (g.m + 31) >> 5;
     for (int i = threadIdx.x; i < mw * kTile; i += blockDim.x) par[i] = 0u;
-    if (threadIdx.x < kTile) cnt_lds[threadIdx.x] = 0;
+    if (threadIdx.x < kTile) {
+        cnt_lds[threadIdx.x] = 0;
+        err_lds[threadIdx.x] = 0;
+    }
     __syncthreads();
 
     const int lane = threadIdx.x & 63;
@@ -292,6 +313,13 @@ __global__ __launch_bounds__(1024) void vn_kernel(DevGraph g, DevState st, int i
     const int nwaves = blockDim.x >> 6;
     const int f = tile * kTile + lane;
     const bool live = st.done[f] == 0;
+    const int itl = kStream ? st.iters[f] : it;  // this lane's iteration
+    const bool lastl = kStream ? (itl == last - 1) : (last != 0);
+    // error bits are only needed by a frame that may fail at this iteration
+    const bool want_err = kStream && __ballot(live && lastl) != 0ull;
+    const int kw = (g.k + 31) >> 5;
+    const uint32_t *Ut = st.ubits + (size_t)tile * kw * kTile + lane;
+    int my_err = 0;
     const double *Et = st.E + (size_t)tile * g.nnz * kTile + lane;
     double *Lt = st.L + (size_t)tile * g.n * kTile + lane;
     const double *Ct = st.ch + (size_t)tile * g.n * kTile + lane;
@@ -320,6 +348,8 @@ __global__ __launch_bounds__(1024) void vn_kernel(DevGraph g, DevState st, int i
             const double ap = kFirst ? chj : Lt[j * kTile];  // a-priori = previous L (:274)
             my_cnt += (fabs(Lj) <= 7.0 && ap * Lj < 0.0) ? 1 : 0;
         }
+        if (want_err && j < g.k)
+            my_err += (int)(((Ut[(j >> 5) * kTile] >> (j & 31)) & 1u) ^ (Lj < 0.0 ? 0u : 1u));  // u vs z^1
         if (live) Lt[j * kTile] = Lj;
         if (!(Lj < 0.0)) {  // z^1 == 1 -> flips the parity of every row of column j
             for (int p = p0; p < p1; ++p) {
@@ -329,13 +359,43 @@ __global__ __launch_bounds__(1024) void vn_kernel(DevGraph g, DevState st, int i
         }
     }
     if (nllr) atomicAdd(&cnt_lds[lane], my_cnt);
+    if (want_err) atomicAdd(&err_lds[lane], my_err);
     __syncthreads();
     if (wave != 0) return;
 
     uint32_t acc = 0u;
     for (int w = 0; w < mw; ++w) acc |= par[w * kTile + lane];
     bool still = false;
-    if (live) {
+    if (kStream) {
+        unsigned long long v[7] = {0, 0, 0, 0, 0, 0, 0};
+        bool fin = false;
+        if (live) {
+            const bool ok = acc == 0u;
+            fin = ok || lastl;
+            if (fin) {
+                v[0] = 1;
+                v[1] = ok ? 0 : 1;
+                v[2] = ok ? 0 : (unsigned long long)err_lds[lane];
+                v[3] = ok ? (unsigned long long)itl : 0;
+                v[4] = ok ? 1 : 0;
+                v[5] = nllr ? (unsigned long long)cnt_lds[lane] : 0;
+                v[6] = (unsigned long long)(itl + 1);
+                st.done[f] = 1;
+                st.refill[f] = 1;
+            } else {
+                st.iters[f] = itl + 1;
+                still = true;
+            }
+            st.fresh[f] = 0;
+        }
+        if (__ballot(fin) != 0ull) {
+#pragma unroll
+            for (int i = 0; i < 7; ++i) {
+                const unsigned long long s = wave_sum(v[i]);
+                if (lane == 0 && s) atomicAdd(&ctr[i], s);
+            }
+        }
+    } else if (live) {
         if (nllr) {
             const int c = cnt_lds[lane];
             st.nllr_cnt[f] = c;
@@ -370,6 +430,18 @@ __global__ void reset_kernel(DevState st) {
     st.iters[f] = 0;
     st.nllr_cnt[f] = 0;
     if ((f & 63) == 0) st.tile_active[f >> 6] = valid ? 1 : 0;
+}
+
+// Streaming Monte-Carlo: every lane empty and asking for a frame.
+__global__ void stream_init_kernel(DevState st) {
+    const int f = blockIdx.x * blockDim.x + threadIdx.x;
+    if (f >= st.ntiles * kTile) return;
+    st.done[f] = 1;
+    st.refill[f] = 1;
+    st.fresh[f] = 0;
+    st.iters[f] = 0;
+    st.nllr_cnt[f] = 0;
+    if ((f & 63) == 0) st.tile_active[f >> 6] = 0;
 }
 
 // llr [count][n] (row per frame) -> ch [tile][n][64]
@@ -414,15 +486,13 @@ __device__ __forceinline__ double u52(uint32_t hi, uint32_t lo) {
     return ((double)x + 0.5) * 0x1p-52;                    // exact, in (0,1)
 }
 
-__global__ __launch_bounds__(64) void generate_kernel(DevGraph g, DevState st, uint64_t seed, int snr_point,
-                                                      double sigma, int64_t frame0,
-                                                      const uint32_t *__restrict__ apack) {
-    extern __shared__ uint32_t ul[];
-    const int tile = blockIdx.x;
-    const int lane = threadIdx.x;
-    const int f = tile * kTile + lane;
+// Frame F of SNR point `snr_point` into lane `lane` of `tile`: info bits (ubits
+// and the lane's LDS column `ul`), channel LLRs ch[tile][j][lane].  With
+// `set_L`, also L = ch (a streaming refill: the next CN then forms M = L - 0).
+__device__ void gen_lane(const DevGraph &g, const DevState &st, int tile, int lane, int64_t F, uint64_t seed,
+                         int snr_point, double sigma, const uint32_t *__restrict__ apack, uint32_t *ul, bool valid,
+                         bool set_L) {
     const int kw = (g.k + 31) >> 5;
-    const int64_t F = frame0 + f;
     const uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
     const uint32_t flo = (uint32_t)F, fhi = (uint32_t)((uint64_t)F >> 32);
     // info bits: data_buffer.py:23 / generator.py:7-9 (random.randint(0,1) per bit)
@@ -442,6 +512,7 @@ __global__ __launch_bounds__(64) void generate_kernel(DevGraph g, DevState st, u
     // codeword [u, A.u mod 2] + BPSK + AWGN (channel.py:49,68-80)
     const double s2 = sigma * sigma;
     double *Ct = st.ch + (size_t)tile * g.n * kTile + lane;
+    double *Lt = st.L + (size_t)tile * g.n * kTile + lane;
     for (int jb = 0; jb < g.n; jb += 2) {
         uint32_t c[4] = {flo, fhi, (uint32_t)(jb >> 1), ((uint32_t)snr_point << 1) | 1u};
         philox4x32_10(c, k0, k1);
@@ -465,9 +536,53 @@ __global__ __launch_bounds__(64) void generate_kernel(DevGraph g, DevState st, u
             }
             const double x = bit ? 1.0 : -1.0;
             const double y = x + s2 * gz[q];
-            Ct[j * kTile] = f < st.count ? (2.0 * y) / s2 : 0.0;
+            const double llr = valid ? (2.0 * y) / s2 : 0.0;
+            Ct[j * kTile] = llr;
+            if (set_L) Lt[j * kTile] = llr;
         }
     }
+}
+
+__global__ __launch_bounds__(64) void generate_kernel(DevGraph g, DevState st, uint64_t seed, int snr_point,
+                                                      double sigma, int64_t frame0,
+                                                      const uint32_t *__restrict__ apack) {
+    extern __shared__ uint32_t ul[];
+    const int tile = blockIdx.x;
+    const int lane = threadIdx.x;
+    const int f = tile * kTile + lane;
+    gen_lane(g, st, tile, lane, frame0 + f, seed, snr_point, sigma, apack, ul, f < st.count, false);
+}
+
+// Streaming refill (Monte-Carlo path): every lane flagged by vn_kernel (or, at
+// the start, every lane) takes the next frame index from one device counter
+// (wave-aggregated atomicAdd) and generates it in place; with no frame left the
+// lane goes idle.  Lanes of one tile therefore decode different frames at
+// different iterations -- each lane's state depends on its own frame only.
+__global__ __launch_bounds__(64) void refill_kernel(DevGraph g, DevState st, uint64_t seed, int snr_point,
+                                                    double sigma, int64_t frame0, int64_t total,
+                                                    unsigned long long *next, const uint32_t *__restrict__ apack) {
+    extern __shared__ uint32_t ul[];
+    const int tile = blockIdx.x;
+    const int lane = threadIdx.x;
+    const int f = tile * kTile + lane;
+    const bool need = st.refill[f] != 0;
+    const unsigned long long want = __ballot(need);
+    if (want == 0ull) return;
+    const unsigned long long below = lane ? (want & (~0ull >> (64 - lane))) : 0ull;
+    unsigned long long base = 0ull;
+    if (lane == __ffsll((long long)want) - 1) base = atomicAdd(next, (unsigned long long)__popcll(want));
+    base = __shfl(base, __ffsll((long long)want) - 1);
+    const int64_t idx = (int64_t)(base + (unsigned long long)__popcll(below));
+    const bool have = need && idx < total;
+    if (have) gen_lane(g, st, tile, lane, frame0 + idx, seed, snr_point, sigma, apack, ul, true, true);
+    if (need) {
+        st.refill[f] = 0;
+        st.done[f] = have ? 0 : 1;
+        st.fresh[f] = have ? 1 : 0;
+        st.iters[f] = 0;
+    }
+    const unsigned long long busy = __ballot(st.done[f] == 0);
+    if (lane == 0) st.tile_active[tile] = busy != 0ull ? 1 : 0;
 }
 
 __global__ void export_frames_kernel(DevGraph g, DevState st, uint8_t *u_out, double *llr_out) {
@@ -483,12 +598,6 @@ __global__ void export_frames_kernel(DevGraph g, DevState st, uint8_t *u_out, do
         const uint32_t w = st.ubits[((size_t)tile * kw + (j >> 5)) * kTile + lane];
         u_out[(size_t)f * g.k + j] = (uint8_t)((w >> (j & 31)) & 1u);
     }
-}
-
-__device__ __forceinline__ unsigned long long wave_sum(unsigned long long v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-    return v;
 }
 
 // Per-frame Monte-Carlo counters (main.py:130-138 + :154-172), one wave per tile.
@@ -545,36 +654,58 @@ hipError_t launch_load_llr(const DevGraph &g, const DevState &st, const double *
     return hipGetLastError();
 }
 
-hipError_t launch_cn(const DevGraph &g, const DevState &st, int it, hipStream_t s) {
+hipError_t launch_cn(const DevGraph &g, const DevState &st, int it, hipStream_t s, bool stream) {
     const int bpt = (g.m + kCnRowsPerBlock - 1) / kCnRowsPerBlock;
     const unsigned grid = (unsigned)(((st.ntiles + 7) / 8) * 8 * bpt);
     const int par = it & 1;
-    if (it == 0)
-        cn_kernel<true><<<grid, 256, cn_lds_pad(), s>>>(g, st, bpt, par, g.col_idx, g.row_ptr);
+    if (stream)
+        cn_kernel<false, true><<<grid, 256, cn_lds_pad(), s>>>(g, st, bpt, par, g.col_idx, g.row_ptr);
+    else if (it == 0)
+        cn_kernel<true, false><<<grid, 256, cn_lds_pad(), s>>>(g, st, bpt, par, g.col_idx, g.row_ptr);
     else
-        cn_kernel<false><<<grid, 256, cn_lds_pad(), s>>>(g, st, bpt, par, g.col_idx, g.row_ptr);
+        cn_kernel<false, false><<<grid, 256, cn_lds_pad(), s>>>(g, st, bpt, par, g.col_idx, g.row_ptr);
     return hipGetLastError();
 }
 
-hipError_t launch_cn_rare(const DevGraph &g, const DevState &st, int it, hipStream_t s) {
+hipError_t launch_cn_rare(const DevGraph &g, const DevState &st, int it, hipStream_t s, bool stream) {
     const unsigned grid = (unsigned)(st.nslots / 4);
     const int par = it & 1;
-    if (it == 0)
-        cn_rare_kernel<true><<<grid, 256, 0, s>>>(g, st, par);
+    if (stream)
+        cn_rare_kernel<false, true><<<grid, 256, 0, s>>>(g, st, par);
+    else if (it == 0)
+        cn_rare_kernel<true, false><<<grid, 256, 0, s>>>(g, st, par);
     else
-        cn_rare_kernel<false><<<grid, 256, 0, s>>>(g, st, par);
+        cn_rare_kernel<false, false><<<grid, 256, 0, s>>>(g, st, par);
     return hipGetLastError();
 }
 
-hipError_t launch_vn(const DevGraph &g, const DevState &st, int it, int max_iter, bool nllr, hipStream_t s) {
+hipError_t launch_vn(const DevGraph &g, const DevState &st, int it, int max_iter, bool nllr, hipStream_t s,
+                     unsigned long long *stream_ctr) {
     const size_t lds = (size_t)((g.m + 31) >> 5) * kTile * sizeof(uint32_t);
     const int last = it == max_iter - 1 ? 1 : 0;
-    if (it == 0)
-        vn_kernel<true><<<st.ntiles, kVnWaves * 64, lds, s>>>(g, st, it, last, nllr ? 1 : 0, g.csc_ptr, g.csc_edge,
-                                                               g.csc_row);
+    const int nl = nllr ? 1 : 0;
+    if (stream_ctr)
+        vn_kernel<false, true><<<st.ntiles, kVnWaves * 64, lds, s>>>(g, st, it, max_iter, nl, g.csc_ptr,
+                                                                      g.csc_edge, g.csc_row, stream_ctr);
+    else if (it == 0)
+        vn_kernel<true, false><<<st.ntiles, kVnWaves * 64, lds, s>>>(g, st, it, last, nl, g.csc_ptr, g.csc_edge,
+                                                                      g.csc_row, nullptr);
     else
-        vn_kernel<false><<<st.ntiles, kVnWaves * 64, lds, s>>>(g, st, it, last, nllr ? 1 : 0, g.csc_ptr, g.csc_edge,
-                                                                g.csc_row);
+        vn_kernel<false, false><<<st.ntiles, kVnWaves * 64, lds, s>>>(g, st, it, last, nl, g.csc_ptr, g.csc_edge,
+                                                                       g.csc_row, nullptr);
+    return hipGetLastError();
+}
+
+hipError_t launch_stream_init(const DevGraph &, const DevState &st, hipStream_t s) {
+    const int total = st.ntiles * kTile;
+    stream_init_kernel<<<grid_for(total, 256), 256, 0, s>>>(st);
+    return hipGetLastError();
+}
+
+hipError_t launch_refill(const DevGraph &g, const DevState &st, uint64_t seed, int snr_point, double sigma,
+                         int64_t frame0, int64_t total, unsigned long long *next, hipStream_t s) {
+    const size_t lds = (size_t)((g.k + 31) >> 5) * kTile * sizeof(uint32_t);
+    refill_kernel<<<st.ntiles, kTile, lds, s>>>(g, st, seed, snr_point, sigma, frame0, total, next, g.a_packed);
     return hipGetLastError();
 }
 

@@ -13,7 +13,7 @@ import numpy as np
 from scipy import sparse
 
 from . import _lib
-from ._lib import LDPC_F_NLLR, LDPC_MC_NCOUNT, as_i32, check
+from ._lib import LDPC_F_NLLR, LDPC_F_STATIC, LDPC_MC_NCOUNT, as_i32, check
 
 
 def _csr_arrays(H):
@@ -133,13 +133,18 @@ class Decoder:
             _lib.ptr(u), _lib.ptr(llr), None))
         return u, llr
 
-    def mc_run(self, seed, sigmas, frames_per_point, frame0, max_iter, nllr=False):
-        """Generate + decode + count on the GPU; returns int64 [n_points, 7] counters."""
+    def mc_run(self, seed, sigmas, frames_per_point, frame0, max_iter, nllr=False, static=False):
+        """Generate + decode + count on the GPU; returns int64 [n_points, 7] counters.
+
+        Default schedule streams frames through the decoder's slots (a slot is
+        refilled as soon as its frame stops); static=True decodes chunks of
+        capacity frames to completion.  Same frames, identical counters."""
         sig = np.ascontiguousarray(np.asarray(sigmas, dtype=np.float64))
         out = np.zeros((len(sig), LDPC_MC_NCOUNT), np.int64)
+        flags = (LDPC_F_NLLR if nllr else 0) | (LDPC_F_STATIC if static else 0)
         check("ldpc_mc_run", _lib.lib().ldpc_mc_run(
             self._h, int(seed), len(sig), sig.ctypes.data_as(ctypes.POINTER(ctypes.c_double)),
-            int(frames_per_point), int(frame0), int(max_iter), LDPC_F_NLLR if nllr else 0,
+            int(frames_per_point), int(frame0), int(max_iter), flags,
             out.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)), None))
         return out
 

@@ -95,3 +95,39 @@ def test_simulate_end_to_end_results_schema(gpu_available, tmp_path):
     res.to_json(tmp_path / "r.json")
     back = SimulationResult.from_json(tmp_path / "r.json")
     assert [sp.fer for sp in back.snr_points] == [sp.fer for sp in res.snr_points]
+
+
+# --- streaming schedule (slots refilled as frames stop) vs the static chunks
+@pytest.mark.parametrize("code,cap,frames,T,snrs", [
+    ("wimax_576_0.5", 256, 2048, 20, [1.0, 2.0, 3.0]),       # ~8 frames per slot, mixed iteration counts
+    ("BCH_7_4_1_strip", 64, 5000, 10, [0.0, 3.0, 6.0]),       # ragged last refill, frames >> slots
+    ("wimax_2304_0.75A", 128, 384, 12, [2.0, 4.0]),           # odd-degree sign quirk: failures at 4 dB
+    ("wimax_576_0.5", 512, 100, 50, [0.0]),                   # fewer frames than slots (one partial tile)
+])
+def test_stream_counters_equal_static(gpu_available, code, cap, frames, T, snrs):
+    dec = _decoder(code, cap)
+    sig = [oracle.sigma_for_snr(s) for s in snrs]
+    stream = dec.mc_run(SEED, sig, frames, 7, T, nllr=True)
+    static = dec.mc_run(SEED, sig, frames, 7, T, nllr=True, static=True)
+    np.testing.assert_array_equal(stream, static)
+    assert (stream[:, 0] == frames).all()
+
+
+def test_stream_refills_match_oracle(gpu_available):
+    """Slots decode several frames each; counters == oracle on the same frames."""
+    code, cap, frames, T = "wimax_576_0.5", 128, 640, 10
+    H = hstd_for(code)
+    k = H.shape[1] - H.shape[0]
+    sig = [oracle.sigma_for_snr(2.0)]
+    ctr = _decoder(code, cap).mc_run(SEED, sig, frames, 0, T, nllr=True)
+    u, llr = _decoder(code, frames).generate(SEED, 0, sig[0], 0, frames)
+    o = oracle.spa_decode(H, llr, T, nllr=True)
+    want = oracle.main_counters(u, o["z"], o["status"], o["conv"],
+                                nllr_cnt=np.rint(o["nllr"] * k).astype(np.int64), iters=o["iters"])
+    np.testing.assert_array_equal(ctr[0], want)
+
+
+def test_stream_zero_frames(gpu_available):
+    dec = _decoder("BCH_7_4_1_strip", 64)
+    ctr = dec.mc_run(SEED, [oracle.sigma_for_snr(1.0)], 0, 0, 10)
+    assert not ctr.any()
