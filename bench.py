@@ -52,6 +52,8 @@ def parse():
     ap.add_argument("--mode", choices=("parity", "physical"), default="parity",
                     help="parity: the reference's fp64 decoder on H_std (headline); physical: "
                          "SURVEY §8 f4, standard SPA on the sparse graph, fp32, LDS-resident")
+    ap.add_argument("--phys-hbm", action="store_true",
+                    help="physical mode: HBM-resident state even when a frame fits in LDS")
     ap.add_argument("--dist-backend", default="nccl",
                     help="torch.distributed backend for N>1 ('nccl' = RCCL over xGMI; 'gloo' for "
                          "rehearsing several ranks on one GPU)")
@@ -146,6 +148,36 @@ def cpu_baseline(H, k, args):
             "info_bits_per_s": done * k / dt}
 
 
+def cpu_baseline_phys(H, k, args, ira_code):
+    """Physical mode: its CPU restatement (oracle/phys_oracle.c, one frame per
+    thread call, threads via ctypes which releases the GIL) on a bounded sample."""
+    from concurrent.futures import ThreadPoolExecutor
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle
+    threads = args.cpu_threads or min(16, os.cpu_count() or 1)
+    sigma = oracle.sigma_for_snr(args.snr)
+    Hp, Hgen = H
+
+    def one(i):
+        _, _, llr = oracle.generate_frames(Hgen, SEED, 0, sigma, i * 4, 4, ira=ira_code)
+        return int(oracle.phys_decode(Hp, llr, args.iters)["iters"].sum())
+
+    done, iters, t0, i = 0, 0, time.perf_counter(), 0
+    with ThreadPoolExecutor(threads) as ex:
+        while time.perf_counter() - t0 < args.cpu_seconds:
+            iters += sum(ex.map(one, range(i, i + threads)))
+            done += 4 * threads
+            i += threads
+    dt = time.perf_counter() - t0
+    return {"value": done / dt, "unit": "codewords/s", "cores": threads, "kind": "port",
+            "sample": f"{done} frames of {args.code} (physical mode), T={args.iters}, snr={args.snr} dB "
+                      f"({iters} frame-iterations) in {dt:.1f} s; oracle/phys_oracle.c -O2, {threads} threads",
+            "info_bits_per_s": done * k / dt}
+
+
+IRA_CODES = {"dvbs2_profile_64800_0.5": "dvbs2_profile_matrix"}
+
+
 def main():
     args = parse()
     world, rank, local, dist = dist_setup(args)
@@ -156,13 +188,26 @@ def main():
 
     if ldpc_amd.device_count() <= 0:
         raise SystemExit("bench.py: no HIP device visible (the decoder has no CPU path)")
-    edd = ldpc_amd.load_committed_code(args.code)
-    H = edd._h_std
-    n, m, k, nnz = edd._n, edd._m, edd._k, H.nnz
-    graph = Graph(H, device=local)
+    ira_code = args.code in IRA_CODES
+    if ira_code:  # BASELINE config 5: sparse (physical) mode only, the IRA graph is its own frame source
+        from ldpc_amd import ira
+        if args.mode != "physical":
+            raise SystemExit(f"bench.py: {args.code} runs in --mode physical only (its H_std has ~5e8 edges)")
+        H = getattr(ira, IRA_CODES[args.code])()
+        m, n = H.shape
+        k, nnz = n - m, H.nnz
+        graph = Graph(H, device=local)
+        pgraph = graph
+        Hphys = H
+    else:
+        edd = ldpc_amd.load_committed_code(args.code)
+        H = edd._h_std
+        n, m, k, nnz = edd._n, edd._m, edd._k, H.nnz
+        graph = Graph(H, device=local)
+        Hphys = edd.physical_matrix() if args.mode == "physical" else None
+        pgraph = Graph(Hphys, device=local) if Hphys is not None else None
     chunk = args.chunk or args.frames
     dec = Decoder(graph, chunk)
-    pgraph = Graph(edd.physical_matrix(), device=local) if args.mode == "physical" else None
     sigma = 1.0 / math.sqrt(2.0 * 1.0 * (10.0 ** (args.snr * 0.1)))  # channel.py:113
     B = args.frames
 
@@ -171,7 +216,7 @@ def main():
     def step(s, record=False):
         frame0 = (s * world + rank) * B  # disjoint global frame ranges per rank and step
         if pgraph is not None:
-            c = dec.phys_mc_run(pgraph, SEED, [sigma], B, frame0, args.iters)
+            c = dec.phys_mc_run(pgraph, SEED, [sigma], B, frame0, args.iters, hbm=args.phys_hbm)
         else:
             c = dec.mc_run(SEED, [sigma], B, frame0, args.iters, static=args.schedule == "static")
         if record:
@@ -252,15 +297,44 @@ def main():
                             "count_ms": prof["count"][0]},
         "cpu_baseline": None,
     }
-    if pgraph is not None:  # physical mode: LDS-resident, no HBM message traffic
+    if pgraph is not None:  # physical mode (not the reference's arithmetic: §8 f4)
+        pnnz = int(pgraph.nnz)
         pms, pl = prof["phys"]
+        cms, cl = prof["phys_cn"]
+        vms, vl = prof["phys_vn"]
+        where = "HBM-resident tiles" if cl else "LDS-resident"
         out["dtype"] = "f32"
-        out["config"]["workload"] = out["config"]["workload"].replace(" SPA,", " SPA physical mode (sparse H[:,perm], sign-consistent, fp32, LDS-resident),")
-        out["config"]["edges_H_phys"] = int(pgraph.nnz)
-        out["roofline"] = {"bound": "valu", "kernel": "phys_kernel", "launches": pl,
-                           "avg_launch_ms": pms / max(pl, 1), "note": "state in LDS; HBM traffic is the frame input only"}
-        out["decode_roofline"] = {"phys_ms": pms, "gen_ms": prof["generate"][0]}
-    if rank == 0 and world == 1 and args.cpu_seconds > 0 and pgraph is None:
+        out["config"]["workload"] = out["config"]["workload"].replace(
+            " SPA,", f" SPA physical mode (sparse H[:,perm], sign-consistent, fp32, {where}),")
+        out["config"]["edges_H_phys"] = pnnz
+        if ira_code:
+            out["config"]["edges_H_std"] = None
+            out["config"]["code_note"] = ("DVB-S2 rate-1/2 normal-frame profile (n=64800, degrees 8/3/2, check "
+                                          "degree 7, staircase parity) with a seeded address table: ldpc_amd/ira.py")
+        if cl:  # HBM tile path: phys_cn_tile dominates
+            local_iters = int(local_totals[0, 6])
+            cn_bytes = 12.0 * pnnz * local_iters
+            cn_avg_s = (cms / 1e3) / cl
+            achieved = cn_bytes / cl / cn_avg_s / 1e9
+            out["roofline"] = {
+                "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": achieved / HBM_PEAK_GBS, "traffic": None, "kernel": "phys_cn_tile_kernel",
+                "launches": cl, "avg_launch_ms": cn_avg_s * 1e3, "bytes_per_launch": cn_bytes / cl,
+                "bytes_model": "12 B x H edges x frame-iterations (L[col] gather + E_old read + E_new write, fp32)",
+            }
+            dec_bytes = (16.0 * pnnz + 12.0 * n) * local_iters
+            out["decode_roofline"] = {"achieved_GBs": dec_bytes / ((cms + vms) / 1e3) / 1e9,
+                                      "frac": dec_bytes / ((cms + vms) / 1e3) / 1e9 / HBM_PEAK_GBS,
+                                      "phys_cn_ms": cms, "phys_vn_ms": vms, "gen_ms": prof["generate"][0],
+                                      "count_ms": prof["count"][0]}
+        else:
+            out["roofline"] = {"bound": "valu", "kernel": "phys_kernel", "launches": pl,
+                               "avg_launch_ms": pms / max(pl, 1),
+                               "note": "state in LDS; HBM traffic is the frame input only"}
+            out["decode_roofline"] = {"phys_ms": pms, "gen_ms": prof["generate"][0]}
+        if rank == 0 and world == 1 and args.cpu_seconds > 0:
+            out["cpu_baseline"] = cpu_baseline_phys((Hphys, H), k, args, ira_code)
+    elif rank == 0 and world == 1 and args.cpu_seconds > 0:
         out["cpu_baseline"] = cpu_baseline(H, k, args)
     if rank == 0:
         print(json.dumps(out), flush=True)

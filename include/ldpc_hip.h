@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define LDPC_ABI_VERSION 1
+#define LDPC_ABI_VERSION 2
 
 /* error codes */
 #define LDPC_OK 0
@@ -44,6 +44,7 @@ extern "C" {
 #define LDPC_F_NLLR 0x1u        /* normalized-LLR metric, spa_decoder.py:210-228  */
 #define LDPC_F_DEVICE_PTRS 0x2u /* I/O pointers are device pointers, async        */
 #define LDPC_F_STATIC 0x4u      /* ldpc_mc_run: chunked schedule, no slot refill  */
+#define LDPC_F_PHYS_HBM 0x8u    /* physical mode: HBM-resident state even if LDS fits */
 
 typedef struct ldpc_hstd ldpc_hstd;       /* standard-form parity-check matrix  */
 typedef struct ldpc_graph ldpc_graph;     /* H_std uploaded to one GPU          */
@@ -122,7 +123,8 @@ int ldpc_decode_f64(ldpc_decoder *d, int32_t batch, const double *llr, int32_t m
  * Synthetic frame source that replaces DataBuffer(k) + encode + Channel
  * mode 1 (data_buffer.py:16-82, channel.py:38-81, generator.py:7-9) on the GPU:
  *   u  ~ iid bits from Philox4x32-10, key (seed), counter (frame, snr_point, block, 0)
- *   c  = [u, A.u mod 2]  (H_std = [A | I_m])
+ *   c  = [u, A.u mod 2]  (H_std = [A | I_m]), or for an IRA graph
+ *        H = [H_info | staircase]: c = [u, p], p_r = p_{r-1} ^ (H_info u)_r
  *   x  = BPSK, bit 0 -> -1, bit 1 -> +1          (channel.py:49)
  *   y  = x + sigma^2 * g,  g ~ N(0,1) Box-Muller  (channel.py:68-76: noise std is sigma^2)
  *   llr = 2 y / sigma^2                           (channel.py:80)
@@ -154,18 +156,23 @@ int ldpc_mc_run(ldpc_decoder *d, uint64_t seed, int32_t n_points, const double *
  * NOT the reference's arithmetic.  Standard sum-product on a SPARSE graph --
  * pass H[:, perm] (the ALIST matrix in H_std column order, same code) to
  * ldpc_graph_create -- with the sign convention made consistent with the tanh
- * rule (Lambda = -llr), fp32, every frame's state resident in LDS (one
- * workgroup per frame).  Inputs/outputs keep the reference's conventions:
- * llr as produced by channel.py, z = (bit estimate) ^ 1, status 0 = OK.
- * Fails with LDPC_ERANGE when a frame's state does not fit in LDS.
+ * rule (Lambda = -llr), fp32.  A frame's state lives in LDS (one workgroup per
+ * frame) when it fits (ldpc_phys_lds_bytes <= ~159 KB), otherwise -- or with
+ * LDPC_F_PHYS_HBM -- in HBM, 64 frames per tile (csrc/phys_tile.hip); both
+ * paths compute bit-identical results.  Inputs/outputs keep the reference's
+ * conventions: llr as produced by channel.py, z = (bit estimate) ^ 1,
+ * status 0 = OK.  The HBM path of ldpc_phys_decode synchronises before it
+ * returns (it uses a temporary workspace), also with LDPC_F_DEVICE_PTRS.
  */
 int64_t ldpc_phys_lds_bytes(const ldpc_graph *g);
 int ldpc_phys_decode(const ldpc_graph *g, int32_t batch, const double *llr, int32_t max_iter, uint32_t flags,
                      uint8_t *z_out, int32_t *conv_out, int32_t *status_out, int32_t *iters_out, float *post_out,
                      void *stream);
-/* On-device frames from d_std (its graph must be the matching H_std = [A|I]:
- * same generator as ldpc_mc_run), decoded in physical mode on g_phys;
- * counters as ldpc_mc_run (slot [5] unused). */
+/* On-device frames decoded in physical mode on g_phys; counters as
+ * ldpc_mc_run (slot [5] unused).  The frame source is d_std's graph: either
+ * the code's H_std = [A|I] (same generator as ldpc_mc_run), or -- for an IRA
+ * code H = [H_info | staircase] such as the DVB-S2-profile code -- g_phys
+ * itself (d_std created on g_phys; parities by accumulation). */
 int ldpc_phys_mc_run(ldpc_decoder *d_std, const ldpc_graph *g_phys, uint64_t seed, int32_t n_points,
                      const double *sigmas, int64_t frames_per_point, int64_t frame0, int32_t max_iter,
                      uint32_t flags, int64_t *counters_out, void *stream);
@@ -182,7 +189,9 @@ int ldpc_phys_mc_run(ldpc_decoder *d_std, const ldpc_graph *g_phys, uint64_t see
 #define LDPC_K_GEN 2
 #define LDPC_K_COUNT 3
 #define LDPC_K_PHYS 4
-#define LDPC_K_NKINDS 5
+#define LDPC_K_PHYS_CN 5
+#define LDPC_K_PHYS_VN 6
+#define LDPC_K_NKINDS 7
 int ldpc_profile_enable(ldpc_decoder *d, int enable);
 int ldpc_profile_read(ldpc_decoder *d, double *ms_out, int64_t *launches_out);
 

@@ -18,6 +18,7 @@
 
 using ldpc::DevGraph;
 using ldpc::DevState;
+using ldpc::PhysTile;
 using ldpc::kTile;
 
 static thread_local std::string g_last_error;
@@ -59,6 +60,13 @@ struct ldpc_decoder {
     // staging for host I/O
     double *llr_stage = nullptr, *post_stage = nullptr;
     uint8_t *z_stage = nullptr;
+    // physical mode, HBM-resident state (phys_tile.hip); allocated on first use
+    float *pE = nullptr, *pL = nullptr, *pLam = nullptr;
+    int64_t pE_cap = 0;  // floats in pE
+    int *pbad = nullptr;
+    uint32_t *pbits = nullptr;
+    int *pactive = nullptr;  // [pactive_cap] tiles still running after VN(it)
+    int pactive_cap = 0;
     unsigned long long *counters = nullptr;  // [counters_cap] + 1 frame-index counter (streaming)
     int counters_cap = 0;
     DevState st{};
@@ -117,6 +125,36 @@ int ensure_messages(ldpc_decoder *d) {
         d->E = nullptr;
     }
     return rc;
+}
+
+// IRA generator scratch (parity words) and physical-mode tile state for graph P
+// (E32 sized by P's edges: P may differ from the decoder's own graph).
+int ensure_pbits(ldpc_decoder *d, const DevGraph &P) {
+    if (d->pbits) return LDPC_OK;
+    const size_t mw = (size_t)(P.m + 31) / 32, mw32 = (mw + 31) / 32;
+    return dev_alloc(&d->pbits, (size_t)d->cap_tiles * (mw + mw32) * kTile);  // pbits + wpar
+}
+
+int ensure_phys_tile(ldpc_decoder *d, const DevGraph &P) {
+    const size_t cap = (size_t)d->cap_tiles * kTile;
+    const int64_t need = (int64_t)(cap * (size_t)P.nnz);
+    if (d->pE_cap < need) {
+        (void)hipFree(d->pE);
+        d->pE = nullptr;
+        d->pE_cap = 0;
+        if (int rc = dev_alloc(&d->pE, (size_t)need)) return rc;
+        d->pE_cap = need;
+    }
+    if (!d->pL && dev_alloc(&d->pL, cap * (size_t)d->g->dg.n)) return LDPC_ENOMEM;
+    if (!d->pLam && dev_alloc(&d->pLam, cap * (size_t)d->g->dg.n)) return LDPC_ENOMEM;
+    if (!d->pbad && dev_alloc(&d->pbad, 2 * cap)) return LDPC_ENOMEM;
+    return LDPC_OK;
+}
+
+PhysTile phys_tile(ldpc_decoder *d) {
+    const DevGraph &G = d->g->dg;
+    uint32_t *wpar = d->pbits ? d->pbits + (size_t)d->cap_tiles * ((G.m + 31) / 32) * kTile : nullptr;
+    return PhysTile{d->pE, d->pL, d->pLam, d->pbad, d->pbits, wpar, d->cap_tiles * kTile};
 }
 
 void state_bind(ldpc_decoder *d, int ntiles, int count) {
@@ -264,6 +302,14 @@ int ldpc_graph_create(int32_t m, int32_t n, const int32_t *row_ptr, const int32_
             if (col_idx[e] >= k) hits += (col_idx[e] == k + r) ? 1 : 100;
         std_form = hits == 1;
     }
+    // IRA form: the parity columns are exactly the staircase p_r in rows r, r+1
+    int ira = k > 0 && !std_form;
+    for (int r = 0; r < m && ira; ++r) {
+        int hits = 0;
+        for (int e = row_ptr[r]; e < row_ptr[r + 1]; ++e)
+            if (col_idx[e] >= k) hits += (col_idx[e] == k + r || (r > 0 && col_idx[e] == k + r - 1)) ? 1 : 100;
+        ira = hits == (r > 0 ? 2 : 1);
+    }
     g->device = device;
     DeviceGuard dg(device);
     if (device < 0) (void)hipGetDevice(&g->device);
@@ -281,6 +327,7 @@ int ldpc_graph_create(int32_t m, int32_t n, const int32_t *row_ptr, const int32_
     G.max_row_deg = max_row;
     G.max_col_deg = max_col;
     G.std_form = std_form;
+    G.ira = ira;
     G.row_ptr = p;
     p += m + 1;
     G.col_idx = p;
@@ -389,6 +436,12 @@ int ldpc_decoder_destroy(ldpc_decoder *d) {
     (void)hipFree(d->post_stage);
     (void)hipFree(d->z_stage);
     (void)hipFree(d->counters);
+    (void)hipFree(d->pE);
+    (void)hipFree(d->pL);
+    (void)hipFree(d->pLam);
+    (void)hipFree(d->pbad);
+    (void)hipFree(d->pbits);
+    (void)hipFree(d->pactive);
     for (auto &sp : d->spans) {
         (void)hipEventDestroy(sp.a);
         (void)hipEventDestroy(sp.b);
@@ -534,7 +587,8 @@ int ldpc_generate_frames(ldpc_decoder *d, uint64_t seed, int32_t snr_point, doub
                          int32_t count, uint32_t flags, uint8_t *u_out, double *llr_out, void *stream) {
     if (!d) return ldpc_fail(LDPC_EINVAL, "ldpc_generate_frames: NULL decoder");
     const DevGraph &G = d->g->dg;
-    if (!G.std_form) return ldpc_fail(LDPC_EINVAL, "ldpc_generate_frames: graph is not [A | I_m]");
+    if (!G.std_form && !G.ira)
+        return ldpc_fail(LDPC_EINVAL, "ldpc_generate_frames: graph is neither [A | I_m] nor IRA [H_info | staircase]");
     if (count < 0 || count > d->cap_tiles * kTile || snr_point < 0 || frame0 < 0 || !(sigma > 0.0))
         return ldpc_fail(LDPC_EINVAL, "ldpc_generate_frames: bad arguments (count=%d cap=%d)", count,
                          d->cap_tiles * kTile);
@@ -553,7 +607,15 @@ int ldpc_generate_frames(ldpc_decoder *d, uint64_t seed, int32_t snr_point, doub
         u_dev = u_out;
         l_dev = llr_out;
     }
-    HIP_TRY(ldpc::launch_generate(G, d->st, seed, snr_point, sigma, frame0, s));
+    if (G.ira) {
+        if ((rc = ensure_pbits(d, G))) {
+            (void)hipFree(dev_ptrs ? nullptr : u_dev);
+            return rc;
+        }
+        HIP_TRY(ldpc::launch_ira_generate(G, d->st, phys_tile(d), seed, snr_point, sigma, frame0, false, s));
+    } else {
+        HIP_TRY(ldpc::launch_generate(G, d->st, seed, snr_point, sigma, frame0, s));
+    }
     // export writes u only for j<k, at [f][k]: give it the [count][k] buffer
     HIP_TRY(ldpc::launch_export_frames(G, d->st, u_dev, l_dev, s));
     if (!dev_ptrs) {
@@ -679,26 +741,16 @@ int phys_grid(const DevGraph &G) {
     return cus * per_cu;
 }
 
-int phys_check(const ldpc_graph *g, const char *fn) {
-    if (!g) return ldpc_fail(LDPC_EINVAL, "%s: NULL graph", fn);
-    if (ldpc::phys_lds_bytes(g->dg) > kLdsLimit)
-        return ldpc_fail(LDPC_ERANGE, "%s: %zu bytes of per-frame state exceed LDS", fn, ldpc::phys_lds_bytes(g->dg));
-    return LDPC_OK;
-}
 
 }  // namespace
 
 int64_t ldpc_phys_lds_bytes(const ldpc_graph *g) { return g ? (int64_t)ldpc::phys_lds_bytes(g->dg) : -1; }
 
-int ldpc_phys_decode(const ldpc_graph *g, int32_t batch, const double *llr, int32_t max_iter, uint32_t flags,
-                     uint8_t *z_out, int32_t *conv_out, int32_t *status_out, int32_t *iters_out, float *post_out,
-                     void *stream) {
-    if (int rc = phys_check(g, "ldpc_phys_decode")) return rc;
-    if (batch < 0 || max_iter < 1 || (batch > 0 && !llr))
-        return ldpc_fail(LDPC_EINVAL, "ldpc_phys_decode: bad arguments (batch=%d max_iter=%d)", batch, max_iter);
-    if (batch == 0) return LDPC_OK;
-    DeviceGuard dg(g->device);
-    hipStream_t s = (hipStream_t)stream;
+namespace {
+
+int phys_decode_lds(const ldpc_graph *g, int32_t batch, const double *llr, int32_t max_iter, uint32_t flags,
+                    uint8_t *z_out, int32_t *conv_out, int32_t *status_out, int32_t *iters_out, float *post_out,
+                    hipStream_t s) {
     const DevGraph &G = g->dg;
     const size_t n = (size_t)G.n, B = (size_t)batch;
     if (flags & LDPC_F_DEVICE_PTRS) {
@@ -734,22 +786,124 @@ int ldpc_phys_decode(const ldpc_graph *g, int32_t batch, const double *llr, int3
     return rc;
 }
 
+// Decode the frames bound in d->st (channel LLRs in d->ch) on graph P with the
+// HBM-resident tile kernels: up to max_iter CN+VN sweeps, then a syndrome-only
+// sweep.  The host reads the running-tile count after VN(it) for it < 4 and
+// every 4th iteration after, and stops issuing sweeps once it is zero.
+int phys_tile_decode(ldpc_decoder *d, const DevGraph &P, int max_iter, bool from_ch, hipStream_t s) {
+    if (d->pactive_cap < max_iter) {
+        (void)hipFree(d->pactive);
+        d->pactive = nullptr;
+        d->pactive_cap = 0;
+        if (int rc = dev_alloc(&d->pactive, (size_t)max_iter)) return rc;
+        d->pactive_cap = max_iter;
+    }
+    const DevState st = d->st;
+    const PhysTile pt = phys_tile(d);
+    HIP_TRY(hipMemsetAsync(d->pactive, 0, sizeof(int) * max_iter, s));
+    HIP_TRY(ldpc::launch_phys_tile_init(P, st, pt, from_ch, s));
+    for (int it = 0; it < max_iter; ++it) {
+        HIP_TRY(timed(d, LDPC_K_PHYS_CN, s, [&] { return ldpc::launch_phys_tile_cn(P, st, pt, it, false, s); }));
+        HIP_TRY(timed(d, LDPC_K_PHYS_VN, s,
+                      [&] { return ldpc::launch_phys_tile_vn(P, st, pt, it, d->pactive, s); }));
+        if (it + 1 < max_iter && (it < 4 || (it + 1) % 4 == 0)) {
+            int running = 0;
+            HIP_TRY(hipMemcpyAsync(&running, d->pactive + it, sizeof(int), hipMemcpyDeviceToHost, s));
+            HIP_TRY(hipStreamSynchronize(s));
+            if (running == 0) break;  // every frame has stopped (converged; final() leaves them alone)
+        }
+    }
+    HIP_TRY(ldpc::launch_phys_tile_cn(P, st, pt, max_iter, true, s));
+    HIP_TRY(ldpc::launch_phys_tile_final(P, st, pt, max_iter, s));
+    return LDPC_OK;
+}
+
+bool phys_use_lds(const DevGraph &P, uint32_t flags) {
+    return !(flags & LDPC_F_PHYS_HBM) && ldpc::phys_lds_bytes(P) <= kLdsLimit;
+}
+
+int phys_decode_tile(const ldpc_graph *g, int32_t batch, const double *llr, int32_t max_iter, uint32_t flags,
+                     uint8_t *z_out, int32_t *conv_out, int32_t *status_out, int32_t *iters_out, float *post_out,
+                     hipStream_t s) {
+    const DevGraph &G = g->dg;
+    const bool dev_ptrs = flags & LDPC_F_DEVICE_PTRS;
+    const int chunk = std::min<int>(batch, 1024);
+    ldpc_decoder *d = nullptr;
+    if (int rc = ldpc_decoder_create(g, chunk, &d)) return rc;
+    struct Free {
+        ldpc_decoder *d;
+        ~Free() { ldpc_decoder_destroy(d); }
+    } guard{d};
+    if (int rc = ensure_phys_tile(d, G)) return rc;
+    const size_t n = (size_t)G.n;
+    for (int start = 0; start < batch; start += chunk) {
+        const int cnt = std::min(chunk, batch - start);
+        state_bind(d, (cnt + kTile - 1) / kTile, cnt);
+        const DevState &st = d->st;
+        const double *src = llr + (size_t)start * n;
+        if (!dev_ptrs) {
+            HIP_TRY(hipMemcpyAsync(d->llr_stage, src, sizeof(double) * cnt * n, hipMemcpyHostToDevice, s));
+            src = d->llr_stage;
+        }
+        HIP_TRY(ldpc::launch_load_llr(G, st, src, s));
+        if (int rc = phys_tile_decode(d, G, max_iter, true, s)) return rc;
+        uint8_t *zd = z_out ? (dev_ptrs ? z_out + (size_t)start * n : d->z_stage) : nullptr;
+        float *pd = post_out ? (dev_ptrs ? post_out + (size_t)start * n : (float *)d->post_stage) : nullptr;
+        HIP_TRY(ldpc::launch_phys_tile_out(G, st, phys_tile(d), zd, pd, s));
+        const hipMemcpyKind kind = dev_ptrs ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost;
+        if (conv_out) HIP_TRY(hipMemcpyAsync(conv_out + start, st.conv, sizeof(int) * cnt, kind, s));
+        if (status_out) HIP_TRY(hipMemcpyAsync(status_out + start, st.status, sizeof(int) * cnt, kind, s));
+        if (iters_out) HIP_TRY(hipMemcpyAsync(iters_out + start, st.iters, sizeof(int) * cnt, kind, s));
+        if (!dev_ptrs) {
+            if (z_out) HIP_TRY(hipMemcpyAsync(z_out + (size_t)start * n, zd, cnt * n, hipMemcpyDeviceToHost, s));
+            if (post_out)
+                HIP_TRY(hipMemcpyAsync(post_out + (size_t)start * n, pd, sizeof(float) * cnt * n,
+                                       hipMemcpyDeviceToHost, s));
+        }
+        HIP_TRY(hipStreamSynchronize(s));  // staging and workspace are reused / freed
+    }
+    return LDPC_OK;
+}
+
+}  // namespace
+
+int ldpc_phys_decode(const ldpc_graph *g, int32_t batch, const double *llr, int32_t max_iter, uint32_t flags,
+                     uint8_t *z_out, int32_t *conv_out, int32_t *status_out, int32_t *iters_out, float *post_out,
+                     void *stream) {
+    if (!g) return ldpc_fail(LDPC_EINVAL, "ldpc_phys_decode: NULL graph");
+    if (batch < 0 || max_iter < 1 || (batch > 0 && !llr))
+        return ldpc_fail(LDPC_EINVAL, "ldpc_phys_decode: bad arguments (batch=%d max_iter=%d)", batch, max_iter);
+    if (batch == 0) return LDPC_OK;
+    DeviceGuard dg(g->device);
+    hipStream_t s = (hipStream_t)stream;
+    if (phys_use_lds(g->dg, flags))
+        return phys_decode_lds(g, batch, llr, max_iter, flags, z_out, conv_out, status_out, iters_out, post_out, s);
+    return phys_decode_tile(g, batch, llr, max_iter, flags, z_out, conv_out, status_out, iters_out, post_out, s);
+}
+
 int ldpc_phys_mc_run(ldpc_decoder *d, const ldpc_graph *gp, uint64_t seed, int32_t n_points, const double *sigmas,
                      int64_t frames_per_point, int64_t frame0, int32_t max_iter, uint32_t flags, int64_t *counters_out,
                      void *stream) {
-    if (int rc = phys_check(gp, "ldpc_phys_mc_run")) return rc;
+    if (!gp) return ldpc_fail(LDPC_EINVAL, "ldpc_phys_mc_run: NULL graph");
     if (!d || n_points <= 0 || !sigmas || frames_per_point < 0 || frame0 < 0 || max_iter < 1 || !counters_out)
         return ldpc_fail(LDPC_EINVAL, "ldpc_phys_mc_run: bad arguments");
     const DevGraph &G = d->g->dg;
     const DevGraph &P = gp->dg;
-    if (!G.std_form) return ldpc_fail(LDPC_EINVAL, "ldpc_phys_mc_run: d_std graph is not [A | I_m]");
+    if (!G.std_form && !(G.ira && d->g == gp))
+        return ldpc_fail(LDPC_EINVAL,
+                         "ldpc_phys_mc_run: the decoder's graph must be the code's H_std = [A | I_m], or the "
+                         "IRA graph itself");
     if (P.n != G.n || P.k != G.k)
         return ldpc_fail(LDPC_EINVAL, "ldpc_phys_mc_run: physical graph shape %dx%d != %dx%d", P.m, P.n, G.m, G.n);
     for (int p = 0; p < n_points; ++p)
         if (!(sigmas[p] > 0.0)) return ldpc_fail(LDPC_EINVAL, "ldpc_phys_mc_run: sigma[%d] <= 0", p);
-    (void)flags;
     DeviceGuard dg(d->g->device);
     hipStream_t s = (hipStream_t)stream;
+    const bool lds = phys_use_lds(P, flags);
+    if (!lds)
+        if (int rc = ensure_phys_tile(d, P)) return rc;
+    if (G.ira)
+        if (int rc = ensure_pbits(d, G)) return rc;
     const int need = n_points * LDPC_MC_NCOUNT;
     if (d->counters_cap < need) {
         (void)hipFree(d->counters);
@@ -761,17 +915,28 @@ int ldpc_phys_mc_run(ldpc_decoder *d, const ldpc_graph *gp, uint64_t seed, int32
     HIP_TRY(hipMemsetAsync(d->counters, 0, sizeof(unsigned long long) * need, s));
     const int64_t cap = (int64_t)d->cap_tiles * kTile;
     for (int p = 0; p < n_points; ++p) {
+        unsigned long long *ctr = d->counters + (size_t)p * LDPC_MC_NCOUNT;
         for (int64_t start = 0; start < frames_per_point; start += cap) {
             const int cnt = (int)std::min<int64_t>(cap, frames_per_point - start);
             state_bind(d, (cnt + kTile - 1) / kTile, cnt);
             const DevState st = d->st;
-            HIP_TRY(timed(d, LDPC_K_GEN, s,
-                          [&] { return ldpc::launch_generate(G, st, seed, p, sigmas[p], frame0 + start, s); }));
-            HIP_TRY(timed(d, LDPC_K_PHYS, s, [&] {
-                return ldpc::launch_phys(P, st.ch, 1, cnt, max_iter, nullptr, nullptr, nullptr, nullptr, nullptr,
-                                         st.ubits, d->counters + (size_t)p * LDPC_MC_NCOUNT,
-                                         std::min(phys_grid(P), cnt), s);
+            // IRA frames for the tile decoder go straight to its fp32 Lambda/L
+            const bool direct = G.ira && !lds;
+            HIP_TRY(timed(d, LDPC_K_GEN, s, [&] {
+                return G.ira ? ldpc::launch_ira_generate(G, st, phys_tile(d), seed, p, sigmas[p], frame0 + start,
+                                                         direct, s)
+                             : ldpc::launch_generate(G, st, seed, p, sigmas[p], frame0 + start, s);
             }));
+            if (lds) {
+                HIP_TRY(timed(d, LDPC_K_PHYS, s, [&] {
+                    return ldpc::launch_phys(P, st.ch, 1, cnt, max_iter, nullptr, nullptr, nullptr, nullptr, nullptr,
+                                             st.ubits, ctr, std::min(phys_grid(P), cnt), s);
+                }));
+            } else {
+                if (int rc = phys_tile_decode(d, P, max_iter, !direct, s)) return rc;
+                HIP_TRY(timed(d, LDPC_K_COUNT, s,
+                              [&] { return ldpc::launch_phys_tile_count(P, st, phys_tile(d), ctr, s); }));
+            }
         }
     }
     std::vector<unsigned long long> h(need);

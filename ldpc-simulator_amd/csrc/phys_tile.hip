@@ -1,0 +1,465 @@
+// phys_tile.hip -- physical mode with the decoder state in HBM, and the IRA
+// frame source (SURVEY.md §8 f4 + BASELINE config 5), gfx950.
+//
+// Same arithmetic as phys_kernels.hip (phys_math.h, identical operation
+// order, so both paths give bit-identical results), for codes whose per-frame
+// state does not fit in LDS (DVB-S2-profile n=64800: E 0.9 MB + L 0.26 MB per
+// frame).  Layout as the parity decoder: 64 frames per tile, lane = frame,
+//   E32 [tile][nnz][64] fp32   L32 [tile][n][64] fp32   ch [tile][n][64] fp64
+// so every load/store of a wavefront is 256 B contiguous.
+//
+//   phys_cn_tile  one wavefront per (tile, 4 check rows): per row, gather
+//                 L[col] and E_old, keep phi(|M|) and the signs of M in
+//                 registers (rows of degree <= kDeg), write E_new: 12 B/edge.
+//                 The same sweep forms the row parity of the hard decisions
+//                 (L < 0) -> bad[it&1][frame]: the syndrome of the previous
+//                 iteration's posterior, for free.
+//   phys_vn_tile  one wavefront per (tile, 8 columns): L = Lambda + sum E
+//                 (Lambda = -channel LLR) in CSC order: 4 B/edge + 12 B/col.
+//                 A frame whose syndrome was zero stops here, converged at
+//                 the previous iteration (exactly the LDS kernel's exit).
+// After the last iteration a syndrome-only CN sweep and phys_tile_final give
+// the frames that converge on it.  Each (tile, row block) and (tile, column
+// block) is placed XCD-aware like cn_kernel.
+//
+// IRA frame source (H = [H_info | staircase], ldpc_amd/ira.py): info words
+// (frame_source.h draws, same as every other generator), s = H_info u
+// (one wavefront per 32 rows -> one word per frame), p = prefix-XOR(s) (one
+// wavefront per tile walks the m/32 words), then BPSK + noise for every
+// column pair.  CPU restatement: oracle/channel_oracle.c (ira == 1).
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "frame_source.h"
+#include "phys_math.h"
+#include "spa_device.h"
+
+namespace ldpc {
+namespace {
+
+constexpr int kRowsPerWave = 4;
+constexpr int kColsPerWave = 8;
+
+__device__ __forceinline__ int uniform(int x) { return __builtin_amdgcn_readfirstlane(x); }
+
+__device__ __forceinline__ unsigned long long wave_sum(unsigned long long v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    return v;
+}
+
+// Work item i = (tile, part).  Blocks b and b+8 run on the same XCD; the grid
+// is a multiple of 8 and block b takes items b, b+G, b+2G, ... so every item
+// of a block -- and every part of one tile -- has the same i%8 = tile%8: a
+// tile's L rows stay in one XCD's L2.  A grid of a few thousand blocks makes
+// a launch over finished tiles cost a few microseconds, not one block per item.
+// bit i of the result = XOR of bits 0..i of x
+__device__ __forceinline__ uint32_t prefix_xor(uint32_t x) {
+    x ^= x << 1;
+    x ^= x << 2;
+    x ^= x << 4;
+    x ^= x << 8;
+    x ^= x << 16;
+    return x;
+}
+
+__device__ __forceinline__ void xcd_item(int i, int per_tile, int &tile, int &part) {
+    const int slot = i >> 3;
+    tile = (slot / per_tile) * 8 + (i & 7);
+    part = slot % per_tile;
+}
+
+// ------------------------------------------------------------ IRA frames
+__global__ __launch_bounds__(64) void ira_ubits_kernel(DevGraph g, DevState st, uint64_t seed, int snr_point,
+                                                       int64_t frame0, int blk_per_block) {
+    const int kw = (g.k + 31) >> 5;
+    const int nblk = (kw + 3) >> 2;
+    const int nbc = (nblk + blk_per_block - 1) / blk_per_block;
+    const int tile = blockIdx.x / nbc, bc = blockIdx.x % nbc;
+    const int lane = threadIdx.x;
+    const int64_t F = frame0 + tile * kTile + lane;
+    const int b1 = min(nblk, (bc + 1) * blk_per_block);
+    for (int blk = bc * blk_per_block; blk < b1; ++blk) {
+        uint32_t c[4];
+        info_block(seed, F, snr_point, blk, c);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int w = blk * 4 + q;
+            if (w >= kw) break;
+            uint32_t v = c[q];
+            if (w == kw - 1 && (g.k & 31)) v &= (1u << (g.k & 31)) - 1u;
+            st.ubits[((size_t)tile * kw + w) * kTile + lane] = v;
+        }
+    }
+}
+
+// s_r = parity of row r's info bits; one wavefront -> 32 rows -> one word,
+// stored as its in-word prefix XOR; the word's total parity (bit 31 of the
+// prefix) is packed into wpar for the carry scan.
+__global__ __launch_bounds__(256) void ira_sbits_kernel(DevGraph g, DevState st, PhysTile pt,
+                                                        const int *__restrict__ row_ptr,
+                                                        const int *__restrict__ col_idx) {
+    const int kw = (g.k + 31) >> 5;
+    const int mw = (g.m + 31) >> 5;
+    const int per_tile = (mw + 3) >> 2;
+    const int tile = blockIdx.x / per_tile;
+    const int w = (blockIdx.x % per_tile) * 4 + uniform(threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (w >= mw) return;
+    const uint32_t *Ut = st.ubits + (size_t)tile * kw * kTile + lane;
+    uint32_t word = 0u;
+    const int r1 = min(g.m, (w + 1) * 32);
+    for (int r = w * 32; r < r1; ++r) {
+        uint32_t b = 0u;
+        for (int e = row_ptr[r]; e < row_ptr[r + 1]; ++e) {
+            const int c = col_idx[e];
+            if (c < g.k) b ^= Ut[(c >> 5) * kTile] >> (c & 31);
+        }
+        word |= (b & 1u) << (r & 31);
+    }
+    const uint32_t x = prefix_xor(word);
+    pt.pbits[((size_t)tile * mw + w) * kTile + lane] = x;
+    const int mw32 = (mw + 31) >> 5;
+    if (x >> 31) atomicOr(&pt.wpar[((size_t)tile * mw32 + (w >> 5)) * kTile + lane], 1u << (w & 31));
+}
+
+// wpar bit w := parity of all s words before word w (exclusive scan), so
+// p_r = bit (r%32) of pbits[r/32] ^ wpar bit (r/32): the staircase accumulator.
+__global__ __launch_bounds__(64) void ira_carry_kernel(DevGraph g, PhysTile pt) {
+    const int mw32 = (((g.m + 31) >> 5) + 31) >> 5;
+    const int tile = blockIdx.x, lane = threadIdx.x;
+    uint32_t *Wt = pt.wpar + (size_t)tile * mw32 * kTile + lane;
+    uint32_t carry = 0u;
+    for (int W = 0; W < mw32; ++W) {
+        const uint32_t z = prefix_xor(Wt[W * kTile]);
+        Wt[W * kTile] = (z << 1) ^ (0u - carry);
+        carry ^= z >> 31;
+    }
+}
+
+// to_lambda: write the decoder's fp32 Lambda = L = -llr directly (physical
+// Monte-Carlo), else the fp64 channel LLRs ch (ldpc_generate_frames).
+__global__ __launch_bounds__(64) void ira_channel_kernel(DevGraph g, DevState st, PhysTile pt, uint64_t seed,
+                                                         int snr_point, double sigma, int64_t frame0,
+                                                         int to_lambda) {
+    const int kw = (g.k + 31) >> 5;
+    const int mw = (g.m + 31) >> 5;
+    const int npairs = (g.n + 1) >> 1;
+    const int per_tile = (npairs + 63) >> 6;
+    const int tile = blockIdx.x / per_tile;
+    const int b0 = (blockIdx.x % per_tile) * 64;
+    const int lane = threadIdx.x;
+    const int f = tile * kTile + lane;
+    const bool valid = f < st.count;
+    const int64_t F = frame0 + f;
+    const double s2 = sigma * sigma;
+    const uint32_t *Ut = st.ubits + (size_t)tile * kw * kTile + lane;
+    const int mw32 = (mw + 31) >> 5;
+    const uint32_t *Pt = pt.pbits + (size_t)tile * mw * kTile + lane;
+    const uint32_t *Wt = pt.wpar + (size_t)tile * mw32 * kTile + lane;
+    double *Ct = st.ch + (size_t)tile * g.n * kTile + lane;
+    float *Lamt = pt.Lam + (size_t)tile * g.n * kTile + lane;
+    float *Lt = pt.L + (size_t)tile * g.n * kTile + lane;
+    const int b1 = min(npairs, b0 + 64);
+    for (int b = b0; b < b1; ++b) {
+        double gz[2];
+        noise_pair(seed, F, snr_point, b, gz);
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+            const int j = 2 * b + q;
+            if (j >= g.n) break;
+            const int r = j - g.k;
+            const int w = r >> 5;
+            const uint32_t bit = j < g.k ? (Ut[(j >> 5) * kTile] >> (j & 31)) & 1u
+                                         : ((Pt[w * kTile] >> (r & 31)) ^ (Wt[(w >> 5) * kTile] >> (w & 31))) & 1u;
+            const double llr = valid ? channel_llr(bit, gz[q], s2) : 0.0;
+            if (to_lambda) {
+                Lamt[j * kTile] = -(float)llr;
+                Lt[j * kTile] = -(float)llr;
+            } else {
+                Ct[j * kTile] = llr;
+            }
+        }
+    }
+}
+
+// ------------------------------------------------------- tile decoder
+__global__ void phys_tile_init_kernel(DevGraph g, DevState st, PhysTile pt, int convert) {
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const size_t total = (size_t)st.ntiles * g.n * kTile;
+    if (convert && i < total) pt.L[i] = pt.Lam[i] = -(float)st.ch[i];  // Lambda = log P0/P1 = -channel LLR
+    if (i < (size_t)st.ntiles * kTile) {
+        const int f = (int)i;
+        const bool valid = f < st.count;
+        st.done[f] = valid ? 0 : 1;
+        st.conv[f] = -1;
+        st.status[f] = 1;
+        st.iters[f] = 0;
+        pt.bad[f] = 0;
+        pt.bad[pt.cap + f] = 0;
+        if ((f & 63) == 0) st.tile_active[f >> 6] = valid ? 1 : 0;
+    }
+}
+
+template <int kDeg>
+__global__ __launch_bounds__(256) void phys_cn_tile_kernel(DevGraph g, DevState st, PhysTile pt, int it,
+                                                           int syn_only, int per_tile, int items,
+                                                           const int *__restrict__ row_ptr,
+                                                           const int *__restrict__ col_idx) {
+    const int lane = threadIdx.x & 63;
+    const int wave = uniform(threadIdx.x >> 6);
+    for (int item = blockIdx.x; item < items; item += gridDim.x) {
+    int tile, part;
+    xcd_item(item, per_tile, tile, part);
+    if (tile >= st.ntiles || !st.tile_active[tile]) continue;
+    const int f = tile * kTile + lane;
+    const bool live = st.done[f] == 0;
+    const float *Lt = pt.L + (size_t)tile * g.n * kTile + lane;
+    float *Et = pt.E + (size_t)tile * g.nnz * kTile + lane;
+    const bool first = it == 0;
+    const bool upd = !syn_only && live;
+    uint32_t bad = 0u;
+    const int r0 = (part * 4 + wave) * kRowsPerWave;
+    for (int rr = 0; rr < kRowsPerWave; ++rr) {
+        const int r = r0 + rr;
+        if (r >= g.m) break;
+        const int beg = row_ptr[r], end = row_ptr[r + 1], deg = end - beg;
+        if (deg == 0) continue;
+        uint32_t hp = 0u;
+        if (deg <= kDeg) {
+            float ph[kDeg];
+            uint32_t sg = 0u;
+            float S = 0.0f;
+#pragma unroll
+            for (int i = 0; i < kDeg; ++i) {
+                if (i < deg) {
+                    // lane-masked loads: a tile with few running frames moves
+                    // only their sectors, not 256 B per wavefront access
+                    const float Lc = live ? Lt[col_idx[beg + i] * kTile] : 0.0f;
+                    hp ^= Lc < 0.0f ? 1u : 0u;
+                    if (!syn_only) {
+                        const float M = (first || !live) ? Lc : Lc - Et[(beg + i) * kTile];
+                        ph[i] = phi(fabsf(M));
+                        S += ph[i];
+                        sg |= (M < 0.0f ? 1u : 0u) << i;
+                    }
+                }
+            }
+            if (upd) {
+                const uint32_t neg = __popc(sg) & 1u;
+#pragma unroll
+                for (int i = 0; i < kDeg; ++i) {
+                    if (i < deg) {
+                        const float mag = phi(fmaxf(S - ph[i], 0.0f));
+                        Et[(beg + i) * kTile] = ((neg ^ (sg >> i)) & 1u) ? -mag : mag;
+                    }
+                }
+            }
+        } else {  // long row: two sweeps, M recomputed (same values)
+            float S = 0.0f;
+            uint32_t neg = 0u;
+            for (int e = beg; e < end; ++e) {
+                const float Lc = live ? Lt[col_idx[e] * kTile] : 0.0f;
+                hp ^= Lc < 0.0f ? 1u : 0u;
+                if (!syn_only) {
+                    const float M = (first || !live) ? Lc : Lc - Et[e * kTile];
+                    S += phi(fabsf(M));
+                    neg ^= (M < 0.0f) ? 1u : 0u;
+                }
+            }
+            if (upd) {
+                for (int e = beg; e < end; ++e) {
+                    const float Lc = Lt[col_idx[e] * kTile];
+                    const float M = first ? Lc : Lc - Et[e * kTile];
+                    const float mag = phi(fmaxf(S - phi(fabsf(M)), 0.0f));
+                    Et[e * kTile] = ((neg ^ ((M < 0.0f) ? 1u : 0u)) != 0u) ? -mag : mag;
+                }
+            }
+        }
+        bad |= hp;
+    }
+    // syndrome of the posterior of iteration it-1 (none before iteration 0)
+    if (it >= 1 && live && bad) pt.bad[(it & 1) * pt.cap + f] = 1;
+    }
+}
+
+__global__ __launch_bounds__(256) void phys_vn_tile_kernel(DevGraph g, DevState st, PhysTile pt, int it,
+                                                           int per_tile, int items, const int *__restrict__ csc_ptr,
+                                                           const int *__restrict__ csc_edge, int *active_count) {
+    const int lane = threadIdx.x & 63;
+    const int wave = uniform(threadIdx.x >> 6);
+    for (int item = blockIdx.x; item < items; item += gridDim.x) {
+    int tile, part;
+    xcd_item(item, per_tile, tile, part);
+    if (tile >= st.ntiles || !st.tile_active[tile]) continue;
+    const int f = tile * kTile + lane;
+    // done[f] may flip to 1 under us (the wave below): either value gives upd = 0
+    const bool live = st.done[f] == 0;
+    const bool conv_now = live && it >= 1 && pt.bad[(it & 1) * pt.cap + f] == 0;
+    const bool upd = live && !conv_now;
+    const float *Et = pt.E + (size_t)tile * g.nnz * kTile + lane;
+    float *Lt = pt.L + (size_t)tile * g.n * kTile + lane;
+    const float *Lamt = pt.Lam + (size_t)tile * g.n * kTile + lane;
+    if (__ballot(upd) != 0ull) {
+        const int j0 = (part * 4 + wave) * kColsPerWave;
+        const int j1 = min(g.n, j0 + kColsPerWave);
+        for (int j = j0; j < j1; ++j) {
+            if (upd) {  // lane-masked: converged / finished frames move no data
+                float s = Lamt[j * kTile];
+                for (int p = csc_ptr[j]; p < csc_ptr[j + 1]; ++p) s += Et[csc_edge[p] * kTile];
+                Lt[j * kTile] = s;
+            }
+        }
+    }
+    if (part == 0 && wave == 0) {
+        if (conv_now) {  // syndrome of iteration it-1 was zero
+            st.done[f] = 1;
+            st.conv[f] = it - 1;
+            st.status[f] = 0;
+            st.iters[f] = it;
+        }
+        pt.bad[((it + 1) & 1) * pt.cap + f] = 0;  // for the next CN sweep
+        const unsigned long long any = __ballot(upd);
+        if (lane == 0) {
+            st.tile_active[tile] = any != 0ull ? 1 : 0;
+            if (any) atomicAdd(&active_count[it], 1);  // host polls: 0 -> every frame has stopped
+        }
+    }
+    }
+}
+
+// after the syndrome-only sweep of "iteration" max_iter
+__global__ void phys_tile_final_kernel(DevState st, PhysTile pt, int max_iter) {
+    const int f = blockIdx.x * blockDim.x + threadIdx.x;
+    if (f >= st.ntiles * kTile || st.done[f]) return;
+    const bool ok = pt.bad[(max_iter & 1) * pt.cap + f] == 0;
+    st.done[f] = 1;
+    st.conv[f] = ok ? max_iter - 1 : -1;
+    st.status[f] = ok ? 0 : 1;
+    st.iters[f] = max_iter;
+}
+
+// L32 tiles -> row-major z = (L < 0 ? 0 : 1) (bit estimate ^ 1) and post
+__global__ void phys_tile_out_kernel(DevGraph g, DevState st, PhysTile pt, uint8_t *z, float *post) {
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= (size_t)st.count * g.n) return;
+    const int f = (int)(i / g.n);
+    const int j = (int)(i % g.n);
+    const float L = pt.L[((size_t)(f >> 6) * g.n + j) * kTile + (f & 63)];
+    if (z) z[i] = L < 0.0f ? 0 : 1;
+    if (post) post[i] = L;
+}
+
+// main.py counters; block = one wavefront x (tile, 1024 info columns)
+__global__ __launch_bounds__(64) void phys_tile_count_kernel(DevGraph g, DevState st, PhysTile pt,
+                                                             unsigned long long *ctr) {
+    const int kw = (g.k + 31) >> 5;
+    const int per_tile = (g.k + 1023) >> 10 > 0 ? (g.k + 1023) >> 10 : 1;
+    const int tile = blockIdx.x / per_tile, part = blockIdx.x % per_tile;
+    const int lane = threadIdx.x;
+    const int f = tile * kTile + lane;
+    const bool valid = f < st.count;
+    const bool failed = valid && st.status[f] != 0;
+    unsigned long long err = 0;
+    if (__ballot(failed) != 0ull) {  // BER counts failed frames only (main.py:130-138)
+        const uint32_t *Ut = st.ubits + (size_t)tile * kw * kTile + lane;
+        const float *Lt = pt.L + (size_t)tile * g.n * kTile + lane;
+        const int j1 = min(g.k, (part + 1) * 1024);
+        for (int j = part * 1024; j < j1; ++j) {
+            const uint32_t u = (Ut[(j >> 5) * kTile] >> (j & 31)) & 1u;
+            err += (u != (Lt[j * kTile] < 0.0f ? 1u : 0u)) ? 1 : 0;
+        }
+        if (!failed) err = 0;
+    }
+    const unsigned long long e = wave_sum(err);
+    if (lane == 0 && e) atomicAdd(&ctr[2], e);
+    if (part != 0) return;
+    const int cv = valid ? st.conv[f] : -1;
+    unsigned long long v[7] = {valid ? 1ull : 0ull, failed ? 1ull : 0ull, 0, cv >= 0 ? (unsigned long long)cv : 0,
+                               cv >= 0 ? 1ull : 0ull, 0, valid ? (unsigned long long)st.iters[f] : 0};
+#pragma unroll
+    for (int i = 0; i < 7; ++i) {
+        if (i == 2 || i == 5) continue;
+        const unsigned long long s = wave_sum(v[i]);
+        if (lane == 0 && s) atomicAdd(&ctr[i], s);
+    }
+}
+
+inline unsigned grid_for(size_t total, int block) { return (unsigned)((total + block - 1) / block); }
+inline unsigned xcd_items(int ntiles, int per_tile) { return (unsigned)(((ntiles + 7) / 8) * 8 * per_tile); }
+// 256 CUs x 16 blocks of 4 waves (a multiple of 8, see xcd_item)
+inline unsigned stride_grid(int items) { return (unsigned)std::min(items, 4096); }
+
+}  // namespace
+
+hipError_t launch_ira_generate(const DevGraph &g, const DevState &st, const PhysTile &pt, uint64_t seed,
+                               int snr_point, double sigma, int64_t frame0, bool to_lambda, hipStream_t s) {
+    const int kw = (g.k + 31) >> 5, mw = (g.m + 31) >> 5;
+    const int nblk = (kw + 3) >> 2, bpb = 16;
+    const int nbc = (nblk + bpb - 1) / bpb;
+    if (g.k > 0) ira_ubits_kernel<<<st.ntiles * nbc, 64, 0, s>>>(g, st, seed, snr_point, frame0, bpb);
+    const int mw32 = (mw + 31) >> 5;
+    hipError_t e = hipMemsetAsync(pt.wpar, 0, sizeof(uint32_t) * (size_t)st.ntiles * mw32 * kTile, s);
+    if (e != hipSuccess) return e;
+    ira_sbits_kernel<<<st.ntiles * ((mw + 3) >> 2), 256, 0, s>>>(g, st, pt, g.row_ptr, g.col_idx);
+    ira_carry_kernel<<<st.ntiles, 64, 0, s>>>(g, pt);
+    const int npairs = (g.n + 1) >> 1;
+    ira_channel_kernel<<<st.ntiles * ((npairs + 63) >> 6), 64, 0, s>>>(g, st, pt, seed, snr_point, sigma, frame0,
+                                                                       to_lambda ? 1 : 0);
+    return hipGetLastError();
+}
+
+hipError_t launch_phys_tile_init(const DevGraph &g, const DevState &st, const PhysTile &pt, bool convert,
+                                 hipStream_t s) {
+    const size_t total = convert ? std::max((size_t)st.ntiles * g.n * kTile, (size_t)st.ntiles * kTile)
+                                 : (size_t)st.ntiles * kTile;
+    phys_tile_init_kernel<<<grid_for(total, 256), 256, 0, s>>>(g, st, pt, convert ? 1 : 0);
+    return hipGetLastError();
+}
+
+hipError_t launch_phys_tile_cn(const DevGraph &g, const DevState &st, const PhysTile &pt, int it, bool syn_only,
+                               hipStream_t s) {
+    const int per_tile = (g.m + 4 * kRowsPerWave - 1) / (4 * kRowsPerWave);
+    const int items = (int)xcd_items(st.ntiles, per_tile);
+    const unsigned grid = stride_grid(items);
+    const int so = syn_only ? 1 : 0;
+    if (g.max_row_deg <= 8)
+        phys_cn_tile_kernel<8><<<grid, 256, 0, s>>>(g, st, pt, it, so, per_tile, items, g.row_ptr, g.col_idx);
+    else if (g.max_row_deg <= 16)
+        phys_cn_tile_kernel<16><<<grid, 256, 0, s>>>(g, st, pt, it, so, per_tile, items, g.row_ptr, g.col_idx);
+    else
+        phys_cn_tile_kernel<32><<<grid, 256, 0, s>>>(g, st, pt, it, so, per_tile, items, g.row_ptr, g.col_idx);
+    return hipGetLastError();
+}
+
+hipError_t launch_phys_tile_vn(const DevGraph &g, const DevState &st, const PhysTile &pt, int it, int *active_count,
+                               hipStream_t s) {
+    const int per_tile = (g.n + 4 * kColsPerWave - 1) / (4 * kColsPerWave);
+    const int items = (int)xcd_items(st.ntiles, per_tile);
+    phys_vn_tile_kernel<<<stride_grid(items), 256, 0, s>>>(g, st, pt, it, per_tile, items, g.csc_ptr, g.csc_edge,
+                                                           active_count);
+    return hipGetLastError();
+}
+
+hipError_t launch_phys_tile_final(const DevGraph &, const DevState &st, const PhysTile &pt, int max_iter,
+                                  hipStream_t s) {
+    phys_tile_final_kernel<<<grid_for((size_t)st.ntiles * kTile, 256), 256, 0, s>>>(st, pt, max_iter);
+    return hipGetLastError();
+}
+
+hipError_t launch_phys_tile_out(const DevGraph &g, const DevState &st, const PhysTile &pt, uint8_t *z, float *post,
+                                hipStream_t s) {
+    const size_t total = (size_t)st.count * g.n;
+    if (total && (z || post)) phys_tile_out_kernel<<<grid_for(total, 256), 256, 0, s>>>(g, st, pt, z, post);
+    return hipGetLastError();
+}
+
+hipError_t launch_phys_tile_count(const DevGraph &g, const DevState &st, const PhysTile &pt,
+                                  unsigned long long *ctr, hipStream_t s) {
+    const int per_tile = std::max(1, (g.k + 1023) >> 10);
+    phys_tile_count_kernel<<<st.ntiles * per_tile, 64, 0, s>>>(g, st, pt, ctr);
+    return hipGetLastError();
+}
+
+}  // namespace ldpc

@@ -25,6 +25,7 @@ struct DevGraph {
     int m, n, k, nnz;
     int max_row_deg, max_col_deg;
     int std_form;            // 1 if H_std = [A | I_m] exactly (encoder usable)
+    int ira;                 // 1 if H = [H_info | staircase] (IRA encoder usable)
     const int *row_ptr;      // [m+1]
     const int *col_idx;      // [nnz]
     const int *csc_ptr;      // [n+1]
@@ -46,6 +47,17 @@ struct DevState {
     int hist_stride;
     int ntiles;              // tiles in this chunk
     int count;               // valid frames in this chunk
+};
+
+// Physical mode with HBM-resident state (phys_tile.hip), same tile layout.
+struct PhysTile {
+    float *E;          // [tile][nnz][64] check->variable messages
+    float *L;          // [tile][n][64] posteriors (Lambda convention: L < 0 -> bit 1)
+    float *Lam;        // [tile][n][64] Lambda = -channel LLR
+    int *bad;          // [2][cap] row-syndrome flags, by iteration parity
+    uint32_t *pbits;   // [tile][m/32][64] IRA: in-word prefix XOR of s = H_info u (generator scratch)
+    uint32_t *wpar;    // [tile][m/1024][64] IRA: bit w = parity of s words before w
+    int cap;           // frames of capacity (stride of bad)
 };
 
 // --- launchers (spa_kernels.hip); all asynchronous on `s` ---
@@ -75,6 +87,25 @@ size_t phys_lds_bytes(const DevGraph &g);
 hipError_t launch_phys(const DevGraph &g, const double *llr, int layout, int count, int max_iter, uint8_t *z,
                        int *conv, int *status, int *iters, float *post, const uint32_t *ubits,
                        unsigned long long *ctr, int grid, hipStream_t s);
+
+// physical mode, HBM-resident tiles + IRA frame source (phys_tile.hip)
+// to_lambda: write fp32 Lambda/L of the tile decoder instead of fp64 ch
+hipError_t launch_ira_generate(const DevGraph &g, const DevState &st, const PhysTile &pt, uint64_t seed,
+                               int snr_point, double sigma, int64_t frame0, bool to_lambda, hipStream_t s);
+// convert: L = Lambda = -(float)ch (else the generator already wrote them)
+hipError_t launch_phys_tile_init(const DevGraph &g, const DevState &st, const PhysTile &pt, bool convert,
+                                 hipStream_t s);
+hipError_t launch_phys_tile_cn(const DevGraph &g, const DevState &st, const PhysTile &pt, int it, bool syn_only,
+                               hipStream_t s);
+// active_count[it] += tiles that still have a running frame after VN(it)
+hipError_t launch_phys_tile_vn(const DevGraph &g, const DevState &st, const PhysTile &pt, int it, int *active_count,
+                               hipStream_t s);
+hipError_t launch_phys_tile_final(const DevGraph &g, const DevState &st, const PhysTile &pt, int max_iter,
+                                  hipStream_t s);
+hipError_t launch_phys_tile_out(const DevGraph &g, const DevState &st, const PhysTile &pt, uint8_t *z, float *post,
+                                hipStream_t s);
+hipError_t launch_phys_tile_count(const DevGraph &g, const DevState &st, const PhysTile &pt,
+                                  unsigned long long *ctr, hipStream_t s);
 
 // --- Philox4x32-10 (Salmon et al., SC'11), shared by host tests and device ---
 __host__ __device__ inline void philox4x32_10(uint32_t c[4], uint32_t k0, uint32_t k1) {

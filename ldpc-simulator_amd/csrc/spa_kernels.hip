@@ -39,6 +39,7 @@
 #include <cstdint>
 #include <cstdlib>
 
+#include "frame_source.h"
 #include "spa_device.h"
 #include "spa_math.h"
 
@@ -481,11 +482,6 @@ __global__ void export_msgs_kernel(DevGraph g, DevState st, double *out) {
 // ------------------------------------------------ on-device frame generation
 // One block of 64 threads per tile; thread = frame.  u bits live in LDS
 // ([kw][64], each lane reads only its own column, so no barrier is needed).
-__device__ __forceinline__ double u52(uint32_t hi, uint32_t lo) {
-    const uint64_t x = (((uint64_t)hi << 32) | lo) >> 12;  // 52 random bits
-    return ((double)x + 0.5) * 0x1p-52;                    // exact, in (0,1)
-}
-
 // Frame F of SNR point `snr_point` into lane `lane` of `tile`: info bits (ubits
 // and the lane's LDS column `ul`), channel LLRs ch[tile][j][lane].  With
 // `set_L`, also L = ch (a streaming refill: the next CN then forms M = L - 0).
@@ -493,12 +489,10 @@ __device__ void gen_lane(const DevGraph &g, const DevState &st, int tile, int la
                          int snr_point, double sigma, const uint32_t *__restrict__ apack, uint32_t *ul, bool valid,
                          bool set_L) {
     const int kw = (g.k + 31) >> 5;
-    const uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
-    const uint32_t flo = (uint32_t)F, fhi = (uint32_t)((uint64_t)F >> 32);
     // info bits: data_buffer.py:23 / generator.py:7-9 (random.randint(0,1) per bit)
     for (int blk = 0; blk * 4 < kw; ++blk) {
-        uint32_t c[4] = {flo, fhi, (uint32_t)blk, (uint32_t)snr_point << 1};
-        philox4x32_10(c, k0, k1);
+        uint32_t c[4];
+        info_block(seed, F, snr_point, blk, c);
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
             const int w = blk * 4 + q;
@@ -514,13 +508,8 @@ __device__ void gen_lane(const DevGraph &g, const DevState &st, int tile, int la
     double *Ct = st.ch + (size_t)tile * g.n * kTile + lane;
     double *Lt = st.L + (size_t)tile * g.n * kTile + lane;
     for (int jb = 0; jb < g.n; jb += 2) {
-        uint32_t c[4] = {flo, fhi, (uint32_t)(jb >> 1), ((uint32_t)snr_point << 1) | 1u};
-        philox4x32_10(c, k0, k1);
-        const double u1 = u52(c[0], c[1]);
-        const double u2 = u52(c[2], c[3]);
-        const double r = sqrt(-2.0 * log(u1));
-        const double th = 6.283185307179586 * u2;
-        const double gz[2] = {r * cos(th), r * sin(th)};
+        double gz[2];
+        noise_pair(seed, F, snr_point, jb >> 1, gz);
 #pragma unroll
         for (int q = 0; q < 2; ++q) {
             const int j = jb + q;
@@ -534,9 +523,7 @@ __device__ void gen_lane(const DevGraph &g, const DevState &st, int tile, int la
                 for (int w = 0; w < kw; ++w) acc ^= ar[w] & ul[w * kTile + lane];
                 bit = (uint32_t)__popc(acc) & 1u;
             }
-            const double x = bit ? 1.0 : -1.0;
-            const double y = x + s2 * gz[q];
-            const double llr = valid ? (2.0 * y) / s2 : 0.0;
+            const double llr = valid ? channel_llr(bit, gz[q], s2) : 0.0;
             Ct[j * kTile] = llr;
             if (set_L) Lt[j * kTile] = llr;
         }

@@ -16,6 +16,7 @@ LIB_PATH = os.environ.get("LDPC_HIP_LIB", os.path.join(_HERE, "libldpc_hip.so"))
 LDPC_F_NLLR = 0x1
 LDPC_F_DEVICE_PTRS = 0x2
 LDPC_F_STATIC = 0x4
+LDPC_F_PHYS_HBM = 0x8
 LDPC_MC_NCOUNT = 7
 
 # every symbol include/ldpc_hip.h declares

@@ -13,7 +13,7 @@ import numpy as np
 from scipy import sparse
 
 from . import _lib
-from ._lib import LDPC_F_NLLR, LDPC_F_STATIC, LDPC_MC_NCOUNT, as_i32, check
+from ._lib import LDPC_F_NLLR, LDPC_F_PHYS_HBM, LDPC_F_STATIC, LDPC_MC_NCOUNT, as_i32, check
 
 
 def _csr_arrays(H):
@@ -64,8 +64,10 @@ class Graph:
             self._h = None
 
 
-def phys_decode(graph, llr, max_iter, post=False):
-    """Physical-mode decode of [B, n] LLRs on a sparse graph (H[:, perm])."""
+def phys_decode(graph, llr, max_iter, post=False, hbm=False):
+    """Physical-mode decode of [B, n] LLRs on a sparse graph (H[:, perm]).
+
+    State in LDS when a frame fits, else in HBM (hbm=True forces HBM)."""
     llr = np.ascontiguousarray(np.atleast_2d(np.asarray(llr, dtype=np.float64)))
     B, n = llr.shape
     if n != graph.n:
@@ -76,7 +78,8 @@ def phys_decode(graph, llr, max_iter, post=False):
     iters = np.empty(B, np.int32)
     Lp = np.empty((B, n), np.float32) if post else None
     check("ldpc_phys_decode", _lib.lib().ldpc_phys_decode(
-        graph.handle, B, _lib.ptr(llr), int(max_iter), 0, _lib.ptr(z), _lib.ptr(conv), _lib.ptr(status),
+        graph.handle, B, _lib.ptr(llr), int(max_iter), LDPC_F_PHYS_HBM if hbm else 0, _lib.ptr(z), _lib.ptr(conv),
+        _lib.ptr(status),
         _lib.ptr(iters), _lib.ptr(Lp), None))
     return DecodeResult(z=z, conv=conv, status=status, iters=iters, post=Lp)
 
@@ -148,17 +151,20 @@ class Decoder:
             out.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)), None))
         return out
 
-    def phys_mc_run(self, phys_graph, seed, sigmas, frames_per_point, frame0, max_iter):
-        """Physical mode (§8 f4): same on-device frames, decoded on the sparse graph."""
+    def phys_mc_run(self, phys_graph, seed, sigmas, frames_per_point, frame0, max_iter, hbm=False):
+        """Physical mode (§8 f4): same on-device frames, decoded on the sparse graph.
+
+        This decoder's graph is the code's H_std (frame source) or, for an IRA
+        code, phys_graph itself.  hbm=True forces the HBM-resident tile path."""
         sig = np.ascontiguousarray(np.asarray(sigmas, dtype=np.float64))
         out = np.zeros((len(sig), LDPC_MC_NCOUNT), np.int64)
         check("ldpc_phys_mc_run", _lib.lib().ldpc_phys_mc_run(
             self._h, phys_graph.handle, int(seed), len(sig), sig.ctypes.data_as(ctypes.POINTER(ctypes.c_double)),
-            int(frames_per_point), int(frame0), int(max_iter), 0,
+            int(frames_per_point), int(frame0), int(max_iter), LDPC_F_PHYS_HBM if hbm else 0,
             out.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)), None))
         return out
 
-    KINDS = ("cn", "vn", "generate", "count", "phys")
+    KINDS = ("cn", "vn", "generate", "count", "phys", "phys_cn", "phys_vn")
 
     def profile(self, enable=True):
         check("ldpc_profile_enable", _lib.lib().ldpc_profile_enable(self._h, 1 if enable else 0))

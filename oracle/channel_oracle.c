@@ -39,68 +39,95 @@ static double u52(uint32_t hi, uint32_t lo) {
     return ((double)x + 0.5) * 0x1p-52;
 }
 
+static void frame_bits(uint32_t k0, uint32_t k1, int64_t F, int snr_point, int k, uint8_t *u) {
+    const uint32_t flo = (uint32_t)F, fhi = (uint32_t)((uint64_t)F >> 32);
+    const int kw = (k + 31) / 32;
+    for (int blk = 0; blk * 4 < kw; ++blk) {
+        uint32_t w[4] = {flo, fhi, (uint32_t)blk, (uint32_t)snr_point << 1};
+        oracle_philox4x32_10(w, k0, k1);
+        for (int q = 0; q < 4; ++q)
+            for (int b = 0; b < 32; ++b) {
+                const int i = (blk * 4 + q) * 32 + b;
+                if (i < k) u[i] = (uint8_t)((w[q] >> b) & 1u);
+            }
+    }
+}
+
+static void frame_channel(uint32_t k0, uint32_t k1, int64_t F, int snr_point, double sigma, int n, const uint8_t *c,
+                          double *llr) {
+    const uint32_t flo = (uint32_t)F, fhi = (uint32_t)((uint64_t)F >> 32);
+    const double s2 = sigma * sigma;
+    for (int jb = 0; jb < n; jb += 2) {
+        uint32_t w[4] = {flo, fhi, (uint32_t)(jb >> 1), ((uint32_t)snr_point << 1) | 1u};
+        oracle_philox4x32_10(w, k0, k1);
+        const double u1 = u52(w[0], w[1]);
+        const double u2 = u52(w[2], w[3]);
+        const double r = sqrt(-2.0 * log(u1));
+        const double th = 6.283185307179586 * u2;
+        const double g[2] = {r * cos(th), r * sin(th)};
+        for (int q = 0; q < 2 && jb + q < n; ++q) {
+            const int j = jb + q;
+            const double x = c[j] ? 1.0 : -1.0;
+            const double y = x + s2 * g[q];
+            llr[j] = (2.0 * y) / s2;
+        }
+    }
+}
+
 /*
- * H_std CSR (m x n, [A | I_m]); frames frame0..frame0+count-1 of SNR point
- * snr_point.  u_out [count][k] (uint8), c_out [count][n] (uint8), llr_out
- * [count][n]; any may be NULL.  Returns 0 or -1.
+ * Frames frame0..frame0+count-1 of SNR point snr_point.  H is CSR (m x n).
+ * ira == 0: H_std = [A | I_m], c = [u, A u mod 2] (generate_kernel).
+ * ira == 1: H = [H_info | staircase], c = [u, p], p_r = p_{r-1} ^ (H_info u)_r
+ *           (csrc/ira_kernels.hip, ldpc_amd/ira.py).
+ * u_out [count][k] (uint8), c_out [count][n] (uint8), llr_out [count][n]; any
+ * may be NULL.  Returns 0 or -1.
  */
-int oracle_generate_frames(int m, int n, const int *row_ptr, const int *col_idx, uint64_t seed,
-                           int snr_point, double sigma, int64_t frame0, int count, uint8_t *u_out,
-                           uint8_t *c_out, double *llr_out) {
+static int generate(int m, int n, const int *row_ptr, const int *col_idx, uint64_t seed, int snr_point,
+                    double sigma, int64_t frame0, int count, int ira, uint8_t *u_out, uint8_t *c_out,
+                    double *llr_out) {
     const int k = n - m;
     if (k < 0 || count < 0 || !(sigma > 0.0)) return -1;
     uint8_t *u = (uint8_t *)malloc((size_t)(k > 0 ? k : 1));
     uint8_t *c = (uint8_t *)malloc((size_t)n);
-    if (!u || !c) {
+    double *l = (double *)malloc(sizeof(double) * (size_t)n);
+    if (!u || !c || !l) {
         free(u);
         free(c);
+        free(l);
         return -1;
     }
     const uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
-    const double s2 = sigma * sigma;
     for (int f = 0; f < count; ++f) {
         const int64_t F = frame0 + f;
-        const uint32_t flo = (uint32_t)F, fhi = (uint32_t)((uint64_t)F >> 32);
-        const int kw = (k + 31) / 32;
-        for (int blk = 0; blk * 4 < kw; ++blk) {
-            uint32_t w[4] = {flo, fhi, (uint32_t)blk, (uint32_t)snr_point << 1};
-            oracle_philox4x32_10(w, k0, k1);
-            for (int q = 0; q < 4; ++q)
-                for (int b = 0; b < 32; ++b) {
-                    const int i = (blk * 4 + q) * 32 + b;
-                    if (i < k) u[i] = (uint8_t)((w[q] >> b) & 1u);
-                }
+        frame_bits(k0, k1, F, snr_point, k, u);
+        memcpy(c, u, (size_t)k);
+        uint8_t acc = 0;
+        for (int r = 0; r < m; ++r) {
+            uint8_t p = 0;
+            for (int e = row_ptr[r]; e < row_ptr[r + 1]; ++e)
+                if (col_idx[e] < k) p ^= u[col_idx[e]];
+            acc = ira ? (uint8_t)(acc ^ p) : p;
+            c[k + r] = acc;
         }
-        for (int j = 0; j < n; ++j) {
-            if (j < k) {
-                c[j] = u[j];
-            } else {
-                const int r = j - k;
-                uint8_t p = 0;
-                for (int e = row_ptr[r]; e < row_ptr[r + 1]; ++e)
-                    if (col_idx[e] < k) p ^= u[col_idx[e]];
-                c[j] = p;
-            }
-        }
-        for (int jb = 0; jb < n; jb += 2) {
-            uint32_t w[4] = {flo, fhi, (uint32_t)(jb >> 1), ((uint32_t)snr_point << 1) | 1u};
-            oracle_philox4x32_10(w, k0, k1);
-            const double u1 = u52(w[0], w[1]);
-            const double u2 = u52(w[2], w[3]);
-            const double r = sqrt(-2.0 * log(u1));
-            const double th = 6.283185307179586 * u2;
-            const double g[2] = {r * cos(th), r * sin(th)};
-            for (int q = 0; q < 2 && jb + q < n; ++q) {
-                const int j = jb + q;
-                const double x = c[j] ? 1.0 : -1.0;
-                const double y = x + s2 * g[q];
-                if (llr_out) llr_out[(size_t)f * n + j] = (2.0 * y) / s2;
-            }
-        }
+        frame_channel(k0, k1, F, snr_point, sigma, n, c, l);
         if (u_out && k > 0) memcpy(u_out + (size_t)f * k, u, (size_t)k);
         if (c_out) memcpy(c_out + (size_t)f * n, c, (size_t)n);
+        if (llr_out) memcpy(llr_out + (size_t)f * n, l, sizeof(double) * (size_t)n);
     }
     free(u);
     free(c);
+    free(l);
     return 0;
+}
+
+int oracle_generate_frames(int m, int n, const int *row_ptr, const int *col_idx, uint64_t seed,
+                           int snr_point, double sigma, int64_t frame0, int count, uint8_t *u_out,
+                           uint8_t *c_out, double *llr_out) {
+    return generate(m, n, row_ptr, col_idx, seed, snr_point, sigma, frame0, count, 0, u_out, c_out, llr_out);
+}
+
+int oracle_ira_generate_frames(int m, int n, const int *row_ptr, const int *col_idx, uint64_t seed,
+                               int snr_point, double sigma, int64_t frame0, int count, uint8_t *u_out,
+                               uint8_t *c_out, double *llr_out) {
+    return generate(m, n, row_ptr, col_idx, seed, snr_point, sigma, frame0, count, 1, u_out, c_out, llr_out);
 }

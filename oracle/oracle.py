@@ -38,6 +38,8 @@ def lib():
                                               vp, vp, vp, vp, vp, vp, vp]
         L.oracle_generate_frames.restype = ctypes.c_int
         L.oracle_generate_frames.argtypes = [i32, i32, vp, vp, u64, i32, dbl, i64, i32, vp, vp, vp]
+        L.oracle_ira_generate_frames.restype = ctypes.c_int
+        L.oracle_ira_generate_frames.argtypes = [i32, i32, vp, vp, u64, i32, dbl, i64, i32, vp, vp, vp]
         L.oracle_philox4x32_10.restype = None
         L.oracle_philox4x32_10.argtypes = [vp, ctypes.c_uint32, ctypes.c_uint32]
         L.oracle_max_threads.restype = ctypes.c_int
@@ -119,14 +121,17 @@ def np_tanh(x):
     return np.array([f(float(v)) for v in np.asarray(x, dtype=np.float64).ravel()]).reshape(np.shape(x))
 
 
-def generate_frames(H_std, seed, snr_point, sigma, frame0, count):
+def generate_frames(H_std, seed, snr_point, sigma, frame0, count, ira=False):
+    """Frames of the on-device source: H_std = [A | I] (c = [u, A u]) or, with
+    ira=True, an IRA H = [H_info | staircase] (c = [u, accumulated parities])."""
     m, n, indptr, indices = _csr(H_std)
     k = n - m
     u = np.empty((count, k), np.uint8)
     c = np.empty((count, n), np.uint8)
     llr = np.empty((count, n), np.float64)
-    rc = lib().oracle_generate_frames(m, n, _p(indptr), _p(indices), int(seed), int(snr_point), float(sigma),
-                                      int(frame0), int(count), _p(u), _p(c), _p(llr))
+    fn = lib().oracle_ira_generate_frames if ira else lib().oracle_generate_frames
+    rc = fn(m, n, _p(indptr), _p(indices), int(seed), int(snr_point), float(sigma),
+            int(frame0), int(count), _p(u), _p(c), _p(llr))
     if rc != 0:
         raise ValueError("oracle_generate_frames rejected its arguments")
     return u, c, llr
