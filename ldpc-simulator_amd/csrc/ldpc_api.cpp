@@ -607,15 +607,11 @@ int ldpc_generate_frames(ldpc_decoder *d, uint64_t seed, int32_t snr_point, doub
         u_dev = u_out;
         l_dev = llr_out;
     }
-    if (G.ira) {
-        if ((rc = ensure_pbits(d, G))) {
-            (void)hipFree(dev_ptrs ? nullptr : u_dev);
-            return rc;
-        }
-        HIP_TRY(ldpc::launch_ira_generate(G, d->st, phys_tile(d), seed, snr_point, sigma, frame0, false, s));
-    } else {
-        HIP_TRY(ldpc::launch_generate(G, d->st, seed, snr_point, sigma, frame0, s));
+    if ((rc = ensure_pbits(d, G))) {
+        (void)hipFree(dev_ptrs ? nullptr : u_dev);
+        return rc;
     }
+    HIP_TRY(ldpc::launch_frames(G, d->st, phys_tile(d), seed, snr_point, sigma, frame0, false, s));
     // export writes u only for j<k, at [f][k]: give it the [count][k] buffer
     HIP_TRY(ldpc::launch_export_frames(G, d->st, u_dev, l_dev, s));
     if (!dev_ptrs) {
@@ -702,7 +698,8 @@ int ldpc_mc_run(ldpc_decoder *d, uint64_t seed, int32_t n_points, const double *
     if (!(flags & LDPC_F_STATIC)) {
         for (int p = 0; p < n_points; ++p)
             if (int rc = mc_stream_point(d, seed, p, sigmas[p], frames_per_point, frame0, max_iter, nllr, s)) return rc;
-    } else
+    } else {
+    if (int rc = ensure_pbits(d, G)) return rc;
     for (int p = 0; p < n_points; ++p) {
         for (int64_t start = 0; start < frames_per_point; start += cap) {
             const int cnt = (int)std::min<int64_t>(cap, frames_per_point - start);
@@ -710,12 +707,14 @@ int ldpc_mc_run(ldpc_decoder *d, uint64_t seed, int32_t n_points, const double *
             HIP_TRY(ldpc::launch_reset(G, d->st, s));
             const DevState st = d->st;
             HIP_TRY(timed(d, LDPC_K_GEN, s,
-                          [&] { return ldpc::launch_generate(G, st, seed, p, sigmas[p], frame0 + start, s); }));
+                          [&] { return ldpc::launch_frames(G, st, phys_tile(d), seed, p, sigmas[p], frame0 + start,
+                                                           false, s); }));
             HIP_TRY(run_iterations(d, G, st, max_iter, nllr, s));
             HIP_TRY(timed(d, LDPC_K_COUNT, s, [&] {
                 return ldpc::launch_count(G, st, d->counters + (size_t)p * LDPC_MC_NCOUNT, s);
             }));
         }
+    }
     }
     std::vector<unsigned long long> h(need);
     HIP_TRY(hipMemcpyAsync(h.data(), d->counters, sizeof(unsigned long long) * need, hipMemcpyDeviceToHost, s));
@@ -902,8 +901,7 @@ int ldpc_phys_mc_run(ldpc_decoder *d, const ldpc_graph *gp, uint64_t seed, int32
     const bool lds = phys_use_lds(P, flags);
     if (!lds)
         if (int rc = ensure_phys_tile(d, P)) return rc;
-    if (G.ira)
-        if (int rc = ensure_pbits(d, G)) return rc;
+    if (int rc = ensure_pbits(d, G)) return rc;
     const int need = n_points * LDPC_MC_NCOUNT;
     if (d->counters_cap < need) {
         (void)hipFree(d->counters);
@@ -920,12 +918,10 @@ int ldpc_phys_mc_run(ldpc_decoder *d, const ldpc_graph *gp, uint64_t seed, int32
             const int cnt = (int)std::min<int64_t>(cap, frames_per_point - start);
             state_bind(d, (cnt + kTile - 1) / kTile, cnt);
             const DevState st = d->st;
-            // IRA frames for the tile decoder go straight to its fp32 Lambda/L
-            const bool direct = G.ira && !lds;
+            // frames for the tile decoder go straight to its fp32 Lambda/L
+            const bool direct = !lds;
             HIP_TRY(timed(d, LDPC_K_GEN, s, [&] {
-                return G.ira ? ldpc::launch_ira_generate(G, st, phys_tile(d), seed, p, sigmas[p], frame0 + start,
-                                                         direct, s)
-                             : ldpc::launch_generate(G, st, seed, p, sigmas[p], frame0 + start, s);
+                return ldpc::launch_frames(G, st, phys_tile(d), seed, p, sigmas[p], frame0 + start, direct, s);
             }));
             if (lds) {
                 HIP_TRY(timed(d, LDPC_K_PHYS, s, [&] {

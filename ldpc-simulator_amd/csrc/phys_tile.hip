@@ -1,5 +1,5 @@
-// phys_tile.hip -- physical mode with the decoder state in HBM, and the IRA
-// frame source (SURVEY.md §8 f4 + BASELINE config 5), gfx950.
+// phys_tile.hip -- physical mode with the decoder state in HBM (SURVEY.md
+// §8 f4, BASELINE config 5), gfx950.
 //
 // Same arithmetic as phys_kernels.hip (phys_math.h, identical operation
 // order, so both paths give bit-identical results), for codes whose per-frame
@@ -21,17 +21,12 @@
 // After the last iteration a syndrome-only CN sweep and phys_tile_final give
 // the frames that converge on it.  Each (tile, row block) and (tile, column
 // block) is placed XCD-aware like cn_kernel.
-//
-// IRA frame source (H = [H_info | staircase], ldpc_amd/ira.py): info words
-// (frame_source.h draws, same as every other generator), s = H_info u
-// (one wavefront per 32 rows -> one word per frame), p = prefix-XOR(s) (one
-// wavefront per tile walks the m/32 words), then BPSK + noise for every
-// column pair.  CPU restatement: oracle/channel_oracle.c (ira == 1).
+// Frames come from frame_kernels.hip (directly as fp32 Lambda/L for IRA
+// codes, else as fp64 ch converted by phys_tile_init).
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
 
-#include "frame_source.h"
 #include "phys_math.h"
 #include "spa_device.h"
 
@@ -54,134 +49,10 @@ __device__ __forceinline__ unsigned long long wave_sum(unsigned long long v) {
 // of a block -- and every part of one tile -- has the same i%8 = tile%8: a
 // tile's L rows stay in one XCD's L2.  A grid of a few thousand blocks makes
 // a launch over finished tiles cost a few microseconds, not one block per item.
-// bit i of the result = XOR of bits 0..i of x
-__device__ __forceinline__ uint32_t prefix_xor(uint32_t x) {
-    x ^= x << 1;
-    x ^= x << 2;
-    x ^= x << 4;
-    x ^= x << 8;
-    x ^= x << 16;
-    return x;
-}
-
 __device__ __forceinline__ void xcd_item(int i, int per_tile, int &tile, int &part) {
     const int slot = i >> 3;
     tile = (slot / per_tile) * 8 + (i & 7);
     part = slot % per_tile;
-}
-
-// ------------------------------------------------------------ IRA frames
-__global__ __launch_bounds__(64) void ira_ubits_kernel(DevGraph g, DevState st, uint64_t seed, int snr_point,
-                                                       int64_t frame0, int blk_per_block) {
-    const int kw = (g.k + 31) >> 5;
-    const int nblk = (kw + 3) >> 2;
-    const int nbc = (nblk + blk_per_block - 1) / blk_per_block;
-    const int tile = blockIdx.x / nbc, bc = blockIdx.x % nbc;
-    const int lane = threadIdx.x;
-    const int64_t F = frame0 + tile * kTile + lane;
-    const int b1 = min(nblk, (bc + 1) * blk_per_block);
-    for (int blk = bc * blk_per_block; blk < b1; ++blk) {
-        uint32_t c[4];
-        info_block(seed, F, snr_point, blk, c);
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const int w = blk * 4 + q;
-            if (w >= kw) break;
-            uint32_t v = c[q];
-            if (w == kw - 1 && (g.k & 31)) v &= (1u << (g.k & 31)) - 1u;
-            st.ubits[((size_t)tile * kw + w) * kTile + lane] = v;
-        }
-    }
-}
-
-// s_r = parity of row r's info bits; one wavefront -> 32 rows -> one word,
-// stored as its in-word prefix XOR; the word's total parity (bit 31 of the
-// prefix) is packed into wpar for the carry scan.
-__global__ __launch_bounds__(256) void ira_sbits_kernel(DevGraph g, DevState st, PhysTile pt,
-                                                        const int *__restrict__ row_ptr,
-                                                        const int *__restrict__ col_idx) {
-    const int kw = (g.k + 31) >> 5;
-    const int mw = (g.m + 31) >> 5;
-    const int per_tile = (mw + 3) >> 2;
-    const int tile = blockIdx.x / per_tile;
-    const int w = (blockIdx.x % per_tile) * 4 + uniform(threadIdx.x >> 6);
-    const int lane = threadIdx.x & 63;
-    if (w >= mw) return;
-    const uint32_t *Ut = st.ubits + (size_t)tile * kw * kTile + lane;
-    uint32_t word = 0u;
-    const int r1 = min(g.m, (w + 1) * 32);
-    for (int r = w * 32; r < r1; ++r) {
-        uint32_t b = 0u;
-        for (int e = row_ptr[r]; e < row_ptr[r + 1]; ++e) {
-            const int c = col_idx[e];
-            if (c < g.k) b ^= Ut[(c >> 5) * kTile] >> (c & 31);
-        }
-        word |= (b & 1u) << (r & 31);
-    }
-    const uint32_t x = prefix_xor(word);
-    pt.pbits[((size_t)tile * mw + w) * kTile + lane] = x;
-    const int mw32 = (mw + 31) >> 5;
-    if (x >> 31) atomicOr(&pt.wpar[((size_t)tile * mw32 + (w >> 5)) * kTile + lane], 1u << (w & 31));
-}
-
-// wpar bit w := parity of all s words before word w (exclusive scan), so
-// p_r = bit (r%32) of pbits[r/32] ^ wpar bit (r/32): the staircase accumulator.
-__global__ __launch_bounds__(64) void ira_carry_kernel(DevGraph g, PhysTile pt) {
-    const int mw32 = (((g.m + 31) >> 5) + 31) >> 5;
-    const int tile = blockIdx.x, lane = threadIdx.x;
-    uint32_t *Wt = pt.wpar + (size_t)tile * mw32 * kTile + lane;
-    uint32_t carry = 0u;
-    for (int W = 0; W < mw32; ++W) {
-        const uint32_t z = prefix_xor(Wt[W * kTile]);
-        Wt[W * kTile] = (z << 1) ^ (0u - carry);
-        carry ^= z >> 31;
-    }
-}
-
-// to_lambda: write the decoder's fp32 Lambda = L = -llr directly (physical
-// Monte-Carlo), else the fp64 channel LLRs ch (ldpc_generate_frames).
-__global__ __launch_bounds__(64) void ira_channel_kernel(DevGraph g, DevState st, PhysTile pt, uint64_t seed,
-                                                         int snr_point, double sigma, int64_t frame0,
-                                                         int to_lambda) {
-    const int kw = (g.k + 31) >> 5;
-    const int mw = (g.m + 31) >> 5;
-    const int npairs = (g.n + 1) >> 1;
-    const int per_tile = (npairs + 63) >> 6;
-    const int tile = blockIdx.x / per_tile;
-    const int b0 = (blockIdx.x % per_tile) * 64;
-    const int lane = threadIdx.x;
-    const int f = tile * kTile + lane;
-    const bool valid = f < st.count;
-    const int64_t F = frame0 + f;
-    const double s2 = sigma * sigma;
-    const uint32_t *Ut = st.ubits + (size_t)tile * kw * kTile + lane;
-    const int mw32 = (mw + 31) >> 5;
-    const uint32_t *Pt = pt.pbits + (size_t)tile * mw * kTile + lane;
-    const uint32_t *Wt = pt.wpar + (size_t)tile * mw32 * kTile + lane;
-    double *Ct = st.ch + (size_t)tile * g.n * kTile + lane;
-    float *Lamt = pt.Lam + (size_t)tile * g.n * kTile + lane;
-    float *Lt = pt.L + (size_t)tile * g.n * kTile + lane;
-    const int b1 = min(npairs, b0 + 64);
-    for (int b = b0; b < b1; ++b) {
-        double gz[2];
-        noise_pair(seed, F, snr_point, b, gz);
-#pragma unroll
-        for (int q = 0; q < 2; ++q) {
-            const int j = 2 * b + q;
-            if (j >= g.n) break;
-            const int r = j - g.k;
-            const int w = r >> 5;
-            const uint32_t bit = j < g.k ? (Ut[(j >> 5) * kTile] >> (j & 31)) & 1u
-                                         : ((Pt[w * kTile] >> (r & 31)) ^ (Wt[(w >> 5) * kTile] >> (w & 31))) & 1u;
-            const double llr = valid ? channel_llr(bit, gz[q], s2) : 0.0;
-            if (to_lambda) {
-                Lamt[j * kTile] = -(float)llr;
-                Lt[j * kTile] = -(float)llr;
-            } else {
-                Ct[j * kTile] = llr;
-            }
-        }
-    }
 }
 
 // ------------------------------------------------------- tile decoder
@@ -392,23 +263,6 @@ inline unsigned xcd_items(int ntiles, int per_tile) { return (unsigned)(((ntiles
 inline unsigned stride_grid(int items) { return (unsigned)std::min(items, 4096); }
 
 }  // namespace
-
-hipError_t launch_ira_generate(const DevGraph &g, const DevState &st, const PhysTile &pt, uint64_t seed,
-                               int snr_point, double sigma, int64_t frame0, bool to_lambda, hipStream_t s) {
-    const int kw = (g.k + 31) >> 5, mw = (g.m + 31) >> 5;
-    const int nblk = (kw + 3) >> 2, bpb = 16;
-    const int nbc = (nblk + bpb - 1) / bpb;
-    if (g.k > 0) ira_ubits_kernel<<<st.ntiles * nbc, 64, 0, s>>>(g, st, seed, snr_point, frame0, bpb);
-    const int mw32 = (mw + 31) >> 5;
-    hipError_t e = hipMemsetAsync(pt.wpar, 0, sizeof(uint32_t) * (size_t)st.ntiles * mw32 * kTile, s);
-    if (e != hipSuccess) return e;
-    ira_sbits_kernel<<<st.ntiles * ((mw + 3) >> 2), 256, 0, s>>>(g, st, pt, g.row_ptr, g.col_idx);
-    ira_carry_kernel<<<st.ntiles, 64, 0, s>>>(g, pt);
-    const int npairs = (g.n + 1) >> 1;
-    ira_channel_kernel<<<st.ntiles * ((npairs + 63) >> 6), 64, 0, s>>>(g, st, pt, seed, snr_point, sigma, frame0,
-                                                                       to_lambda ? 1 : 0);
-    return hipGetLastError();
-}
 
 hipError_t launch_phys_tile_init(const DevGraph &g, const DevState &st, const PhysTile &pt, bool convert,
                                  hipStream_t s) {

@@ -75,8 +75,6 @@ hipError_t launch_refill(const DevGraph &g, const DevState &st, uint64_t seed, i
 hipError_t launch_finalize(const DevGraph &g, const DevState &st, uint8_t *z, double *post,
                            hipStream_t s);
 hipError_t launch_export_msgs(const DevGraph &g, const DevState &st, double *out, hipStream_t s);
-hipError_t launch_generate(const DevGraph &g, const DevState &st, uint64_t seed, int snr_point,
-                           double sigma, int64_t frame0, hipStream_t s);
 hipError_t launch_export_frames(const DevGraph &g, const DevState &st, uint8_t *u_out, double *llr_out,
                                 hipStream_t s);
 hipError_t launch_count(const DevGraph &g, const DevState &st, unsigned long long *counters,
@@ -89,9 +87,11 @@ hipError_t launch_phys(const DevGraph &g, const double *llr, int layout, int cou
                        unsigned long long *ctr, int grid, hipStream_t s);
 
 // physical mode, HBM-resident tiles + IRA frame source (phys_tile.hip)
-// to_lambda: write fp32 Lambda/L of the tile decoder instead of fp64 ch
-hipError_t launch_ira_generate(const DevGraph &g, const DevState &st, const PhysTile &pt, uint64_t seed,
-                               int snr_point, double sigma, int64_t frame0, bool to_lambda, hipStream_t s);
+// on-device frames of a chunk (frame_kernels.hip): info bits -> st.ubits,
+// parities via pt.pbits/pt.wpar (H_std [A|I] or IRA graph), channel LLRs ->
+// st.ch (fp64), or with to_lambda the tile decoder's fp32 Lambda = L = -llr
+hipError_t launch_frames(const DevGraph &g, const DevState &st, const PhysTile &pt, uint64_t seed, int snr_point,
+                         double sigma, int64_t frame0, bool to_lambda, hipStream_t s);
 // convert: L = Lambda = -(float)ch (else the generator already wrote them)
 hipError_t launch_phys_tile_init(const DevGraph &g, const DevState &st, const PhysTile &pt, bool convert,
                                  hipStream_t s);

@@ -479,8 +479,8 @@ __global__ void export_msgs_kernel(DevGraph g, DevState st, double *out) {
     out[i] = st.E[((size_t)(f >> 6) * g.nnz + e) * kTile + (f & 63)];
 }
 
-// ------------------------------------------------ on-device frame generation
-// One block of 64 threads per tile; thread = frame.  u bits live in LDS
+// ------------------------------------------------ per-lane frame generation
+// (streaming refill; whole chunks use frame_kernels.hip).  u bits live in LDS
 // ([kw][64], each lane reads only its own column, so no barrier is needed).
 // Frame F of SNR point `snr_point` into lane `lane` of `tile`: info bits (ubits
 // and the lane's LDS column `ul`), channel LLRs ch[tile][j][lane].  With
@@ -528,16 +528,6 @@ __device__ void gen_lane(const DevGraph &g, const DevState &st, int tile, int la
             if (set_L) Lt[j * kTile] = llr;
         }
     }
-}
-
-__global__ __launch_bounds__(64) void generate_kernel(DevGraph g, DevState st, uint64_t seed, int snr_point,
-                                                      double sigma, int64_t frame0,
-                                                      const uint32_t *__restrict__ apack) {
-    extern __shared__ uint32_t ul[];
-    const int tile = blockIdx.x;
-    const int lane = threadIdx.x;
-    const int f = tile * kTile + lane;
-    gen_lane(g, st, tile, lane, frame0 + f, seed, snr_point, sigma, apack, ul, f < st.count, false);
 }
 
 // Streaming refill (Monte-Carlo path): every lane flagged by vn_kernel (or, at
@@ -705,13 +695,6 @@ hipError_t launch_finalize(const DevGraph &g, const DevState &st, uint8_t *z, do
 hipError_t launch_export_msgs(const DevGraph &g, const DevState &st, double *out, hipStream_t s) {
     const size_t total = (size_t)st.count * g.nnz;
     if (total) export_msgs_kernel<<<grid_for(total, 256), 256, 0, s>>>(g, st, out);
-    return hipGetLastError();
-}
-
-hipError_t launch_generate(const DevGraph &g, const DevState &st, uint64_t seed, int snr_point, double sigma,
-                           int64_t frame0, hipStream_t s) {
-    const size_t lds = (size_t)((g.k + 31) >> 5) * kTile * sizeof(uint32_t);
-    generate_kernel<<<st.ntiles, kTile, lds, s>>>(g, st, seed, snr_point, sigma, frame0, g.a_packed);
     return hipGetLastError();
 }
 
