@@ -118,7 +118,9 @@ def committed_traffic(nnz, frames):
             continue
         t = json.load(open(f))
         if t.get("edges") == nnz and t.get("frames") == frames:
-            best = (t["kernels"]["cn_kernel<false>"]["traffic_bytes"], os.path.relpath(f, ROOT))
+            k = t["kernels"]
+            cn = k.get("cn") or k.get("cn_kernel<false>")
+            best = (cn["traffic_bytes"], os.path.relpath(f, ROOT))
     return best or (None, None)
 
 
@@ -247,6 +249,8 @@ def main():
     # roofline of the dominant kernel (cn_kernel) on THIS rank: algorithmic
     # bytes = 16 B per edge per frame-iteration (read E_old + write E_new)
     cn_ms, cn_launches = prof["cn"]
+    from ldpc_amd import _lib
+    cn_name = _lib.lib().ldpc_cn_kernel_name(graph.handle).decode()
     vn_ms, vn_launches = prof["vn"]
     local_iters = int(local_totals[0, 6])  # this rank's frame-iterations
     cn_bytes_total = 16.0 * nnz * local_iters
@@ -288,7 +292,7 @@ def main():
         "roofline": {
             "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
-            "kernel": "cn_kernel", "launches": cn_launches, "avg_launch_ms": cn_avg_s * 1e3,
+            "kernel": cn_name, "launches": cn_launches, "avg_launch_ms": cn_avg_s * 1e3,
             "bytes_per_launch": cn_bytes_per_launch,
             "bytes_model": "16 B x H_std edges x frame-iterations executed (E_old read + E_new write)",
         },

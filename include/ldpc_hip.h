@@ -83,6 +83,10 @@ void ldpc_hstd_free(ldpc_hstd *h);
 int ldpc_graph_create(int32_t m, int32_t n, const int32_t *row_ptr, const int32_t *col_idx,
                       int32_t device, ldpc_graph **out);
 int ldpc_graph_destroy(ldpc_graph *g);
+/* Name of the check-node kernel the parity decoder launches for this graph
+ * ("cn_row_kernel": rows of degree <= 192 kept in registers, 16 B/edge;
+ * "cn_kernel": one wavefront per row, 24 B/edge) -- measurement labels. */
+const char *ldpc_cn_kernel_name(const ldpc_graph *g);
 int ldpc_graph_info(const ldpc_graph *g, int32_t *m, int32_t *n, int64_t *nnz,
                     int32_t *max_row_deg, int32_t *max_col_deg);
 

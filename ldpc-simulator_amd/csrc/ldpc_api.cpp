@@ -373,6 +373,11 @@ int ldpc_graph_destroy(ldpc_graph *g) {
     return LDPC_OK;
 }
 
+const char *ldpc_cn_kernel_name(const ldpc_graph *g) {
+    if (!g) return "";
+    return ldpc::use_cn_row(g->dg) ? "cn_row_kernel" : "cn_kernel";
+}
+
 int ldpc_graph_info(const ldpc_graph *g, int32_t *m, int32_t *n, int64_t *nnz, int32_t *max_row_deg,
                     int32_t *max_col_deg) {
     if (!g) return ldpc_fail(LDPC_EINVAL, "ldpc_graph_info: NULL graph");

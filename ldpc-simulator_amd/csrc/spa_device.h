@@ -66,6 +66,7 @@ hipError_t launch_load_llr(const DevGraph &g, const DevState &st, const double *
 // stream = the streaming Monte-Carlo schedule (lanes at different iterations,
 // see refill_kernel); stream_ctr != null selects the streaming VN.
 hipError_t launch_cn(const DevGraph &g, const DevState &st, int it, hipStream_t s, bool stream = false);
+bool use_cn_row(const DevGraph &g);  // launch_cn runs cn_row_kernel (else cn_kernel)
 hipError_t launch_cn_rare(const DevGraph &g, const DevState &st, int it, hipStream_t s, bool stream = false);
 hipError_t launch_vn(const DevGraph &g, const DevState &st, int it, int max_iter, bool nllr, hipStream_t s,
                      unsigned long long *stream_ctr = nullptr);

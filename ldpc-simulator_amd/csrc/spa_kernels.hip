@@ -35,6 +35,7 @@
 // (spa_math.h).  Their coefficient tables are staged in LDS per block.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdint>
 #include <cstdlib>
@@ -222,6 +223,103 @@ __global__ __launch_bounds__(256, LDPC_CN_WAVES) void cn_kernel(DevGraph g, DevS
     if (lane == 0) {
         const int at = atomicAdd(&st.rare_count[it_parity], 1);
         st.rare_list[at] = tile * g.m + row;
+    }
+}
+
+// ------------------------------------------------- CN pass, row in registers
+// One workgroup of W = 8 wavefronts per (tile, check row), for rows of degree
+// <= W*K = 192 (every row of wimax_576_0.5).  Wavefront w owns the contiguous
+// edges [beg + w*C, beg + (w+1)*C), C = ceil(deg/W), and keeps their t in
+// registers (K fp64 each, statically indexed):
+//   phase 1  issue all its loads of L[col] and E_old at once (unconditional,
+//            index clamped into the chunk), then t = tanh(M/2)   (8 B/edge read)
+//   phase 2  P = t0*t1*...*t_{deg-1} strictly left to right: wavefront 0
+//            multiplies its chunk, hands the running product to wavefront 1
+//            through LDS, ... (W barriers; the reference's rounding order)
+//   phase 3  E_new = 2 atanh(clip(P/t)) from the register t    (8 B/edge write)
+// = the algorithmic 16 B/edge, and tanh is evaluated once per edge (cn_kernel
+// re-reads E_old and recomputes t in its pass 2).  A row where some lane has
+// |t| <= 1e-10 goes to cn_rare_kernel untouched, as in cn_kernel.
+// A/B on wimax_576_0.5 (tools/ab_cnrow.sh): 11.8 ms vs cn_kernel 14.2 ms;
+// W=4/K=48 (2 waves/SIMD), W=16/K=12, two-stage loads and persistent
+// workgroups were all slower.
+constexpr int kRowW = 8, kRowK = 24;
+template <bool kFirst, bool kStream>
+__global__ __launch_bounds__(64 * kRowW, 4) void cn_row_kernel(DevGraph g, DevState st, int it_parity,
+                                                               const int *__restrict__ col_idx,
+                                                               const int *__restrict__ row_ptr) {
+    constexpr int W = kRowW, K = kRowK;
+    __shared__ MathLds mlds;
+    __shared__ double chain[kTile];  // running product handed from wavefront to wavefront
+    fill_math_lds(mlds);
+    __syncthreads();
+    const LdsTanh ttab{mlds.tanh};
+    const LdsLog ltab{mlds.log};
+    const int lane = threadIdx.x & 63;
+    const int wave = uniform(threadIdx.x >> 6);
+    const int b = blockIdx.x;  // XCD-aware: every row of a tile on the tile's XCD
+    const int slot = b >> 3;
+    const int tile = (slot / g.m) * 8 + (b & 7);
+    const int row = slot % g.m;
+    if (tile >= st.ntiles || !st.tile_active[tile]) return;  // block-uniform
+    const int beg = row_ptr[row], end = row_ptr[row + 1];
+    const int deg = end - beg;
+    if (deg == 0) return;  // spa_decoder.py:115-122
+    const int f = tile * kTile + lane;
+    const bool live = st.done[f] == 0;
+    const bool fresh = kStream && st.fresh[f] != 0;
+    double *Et = st.E + (size_t)tile * g.nnz * kTile + lane;
+    const double *Lt = (kFirst ? st.ch : st.L) + (size_t)tile * g.n * kTile + lane;
+    const int C = (deg + W - 1) / W;
+    const int c0 = beg + wave * C;
+    const int cnt = max(0, min(end, c0 + C) - c0);  // wave-uniform, <= K (host checks deg <= W*K)
+
+    double t[K], eo[K];
+    bool tiny = false;
+    if (cnt > 0) {
+#pragma unroll
+        for (int i = 0; i < K; ++i) {
+            const int e = c0 + min(i, cnt - 1);
+            t[i] = Lt[col_idx[e] * kTile];
+            eo[i] = kFirst ? 0.0 : Et[e * kTile];
+        }
+#pragma unroll
+        for (int i = 0; i < K; ++i) {
+            if (i < cnt) {
+                const double M = kFirst ? t[i] : t[i] - ((kStream && fresh) ? 0.0 : eo[i]);
+                t[i] = cn_tanh(M, ttab);
+                tiny |= !(fabs(t[i]) > kTiny);
+            }
+        }
+    }
+    if (__syncthreads_or(tiny)) {  // rare: the whole row to cn_rare_kernel
+        if (threadIdx.x == 0) {
+            const int at = atomicAdd(&st.rare_count[it_parity], 1);
+            st.rare_list[at] = tile * g.m + row;
+        }
+        return;
+    }
+    for (int w = 0; w < W; ++w) {  // the product chain, in edge order
+        if (wave == w && cnt > 0) {
+            double P = w == 0 ? t[0] : chain[lane];
+#pragma unroll
+            for (int i = 0; i < K; ++i)
+                if (i < cnt && (w != 0 || i != 0)) P = P * t[i];
+            chain[lane] = P;
+        }
+        __syncthreads();
+    }
+    const double P = chain[lane];
+#pragma unroll
+    for (int i = 0; i < K; ++i) {
+        if (i < cnt) {
+#ifdef LDPC_DIAG_NOMATH
+            const double En = P * t[i];
+#else
+            const double En = 2.0 * atanh_f(clip_cl(P / t[i]), ltab);
+#endif
+            if (live) Et[(c0 + i) * kTile] = En;
+        }
     }
 }
 
@@ -631,7 +729,32 @@ hipError_t launch_load_llr(const DevGraph &g, const DevState &st, const double *
     return hipGetLastError();
 }
 
+// cn_row_kernel for rows of degree <= 192; LDPC_CN_ROW=0 forces cn_kernel (A/B)
+bool use_cn_row(const DevGraph &g) {
+    static const int force = [] {
+        const char *e = getenv("LDPC_CN_ROW");
+        return e ? atoi(e) : -1;
+    }();
+    return force != 0 && g.max_row_deg <= kRowW * kRowK;
+}
+
+template <bool kFirst, bool kStream>
+void launch_cn_row(const DevGraph &g, const DevState &st, int par, hipStream_t s) {
+    const unsigned grid = (unsigned)(((st.ntiles + 7) / 8) * 8 * g.m);
+    cn_row_kernel<kFirst, kStream><<<grid, 64 * kRowW, 0, s>>>(g, st, par, g.col_idx, g.row_ptr);
+}
+
 hipError_t launch_cn(const DevGraph &g, const DevState &st, int it, hipStream_t s, bool stream) {
+    if (use_cn_row(g)) {
+        const int par = it & 1;
+        if (stream)
+            launch_cn_row<false, true>(g, st, par, s);
+        else if (it == 0)
+            launch_cn_row<true, false>(g, st, par, s);
+        else
+            launch_cn_row<false, false>(g, st, par, s);
+        return hipGetLastError();
+    }
     const int bpt = (g.m + kCnRowsPerBlock - 1) / kCnRowsPerBlock;
     const unsigned grid = (unsigned)(((st.ntiles + 7) / 8) * 8 * bpt);
     const int par = it & 1;

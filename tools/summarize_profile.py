@@ -34,24 +34,25 @@ def main(src, dst, nnz, frames):
             w.writerow([k, v.get("dispatches"), v.get("FETCH_SIZE"), v.get("WRITE_SIZE")])
     stats = {r["Name"]: r for r in csv.DictReader(open(os.path.join(dst, "kernel_stats.csv")))}
 
-    def find(prefix, table):
-        for k in table:
-            if prefix in k:
-                return k
-        raise KeyError(prefix)
+    def busiest(prefixes, table):
+        """The variant (template instance) of a kernel with the most dispatches."""
+        cands = [k for k in table if any(p in k for p in prefixes)]
+        if not cands:
+            raise KeyError(prefixes)
+        return max(cands, key=lambda k: table[k].get("dispatches", 0))
 
-    vn = find("vn_kernel<false>", agg)
-    vn_alg = 8.0 * nnz * frames  # each message read once
+    cn = busiest(("cn_row_kernel<", "cn_kernel<"), agg)
+    vn = busiest(("vn_kernel<",), agg)
+    vn_alg = 8.0 * nnz * frames  # each message read once (+ ch: n/nnz ~ 1.4 % on 576)
     factor = vn_alg / (agg[vn]["FETCH_SIZE"] * 1024.0)
     out = {"fetch_correction_factor": factor, "frames": frames, "edges": nnz, "kernels": {}}
-    for key in ("cn_kernel<false>", "vn_kernel<false>"):
-        k = find(key, agg)
+    for role, k in (("cn", cn), ("vn", vn)):
         rd = agg[k]["FETCH_SIZE"] * 1024.0 * factor
         wr = agg[k]["WRITE_SIZE"] * 1024.0
-        s = stats[find(key, stats)]
-        out["kernels"][key] = {"read_bytes": rd, "write_bytes": wr, "traffic_bytes": rd + wr,
-                               "avg_ns": float(s["AverageNs"]), "calls": int(s["Calls"]),
-                               "traffic_GBs": (rd + wr) / float(s["AverageNs"])}
+        s = stats[k] if k in stats else next(v for n, v in stats.items() if n.startswith(k[:40]))
+        out["kernels"][role] = {"kernel": k, "read_bytes": rd, "write_bytes": wr, "traffic_bytes": rd + wr,
+                                "avg_ns": float(s["AverageNs"]), "calls": int(s["Calls"]),
+                                "traffic_GBs": (rd + wr) / float(s["AverageNs"])}
     json.dump(out, open(os.path.join(dst, "traffic.json"), "w"), indent=2)
     print(json.dumps(out, indent=2))
 
