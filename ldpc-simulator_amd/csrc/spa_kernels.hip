@@ -55,10 +55,10 @@ constexpr int kPv = 4;                       // VN column-sum loads in flight
 
 __device__ __forceinline__ int uniform(int x) { return __builtin_amdgcn_readfirstlane(x); }
 
-__device__ __forceinline__ double clip_cl(double q) {
-    q = q < -kCL ? -kCL : q;  // np.clip keeps NaN, like these compares
-    return q > kCL ? kCL : q;
-}
+// np.clip(q, -CL, CL) as v_max_f64 + v_min_f64 (2 VALU instead of 2 compares
+// and 4 selects).  Differs from np.clip only for NaN, which a message cannot
+// be for finite or infinite channel LLRs (|t| <= 1, |E| <= 35.04).
+__device__ __forceinline__ double clip_cl(double q) { return fmin(fmax(q, -kCL), kCL); }
 
 // ---- math tables in LDS (9 x 16 tanh pairs + 128 log entries = 6.4 KB)
 struct LdsTanh {
@@ -150,7 +150,7 @@ struct EdgeStream {
 template <bool kFirst, bool kStream>
 __global__ __launch_bounds__(256, LDPC_CN_WAVES) void cn_kernel(DevGraph g, DevState st, int blocks_per_tile,
                                                                 int it_parity, const int *__restrict__ col_idx,
-                                                                const int *__restrict__ row_ptr) {
+                                                                const int *__restrict__ row_ptr, AtanhCoef ac) {
     __shared__ MathLds mlds;
     fill_math_lds(mlds);
     __syncthreads();
@@ -209,7 +209,7 @@ __global__ __launch_bounds__(256, LDPC_CN_WAVES) void cn_kernel(DevGraph g, DevS
 #ifdef LDPC_DIAG_NOMATH
                     const double En = P * t;
 #else
-                    const double En = 2.0 * atanh_f(clip_cl(P / t), ltab);
+                    const double En = 2.0 * atanh_f(clip_cl(P / t), ltab, ac);
 #endif
                     if (live) Et[(e + k) * kTile] = En;
                 }
@@ -240,14 +240,20 @@ __global__ __launch_bounds__(256, LDPC_CN_WAVES) void cn_kernel(DevGraph g, DevS
 // = the algorithmic 16 B/edge, and tanh is evaluated once per edge (cn_kernel
 // re-reads E_old and recomputes t in its pass 2).  A row where some lane has
 // |t| <= 1e-10 goes to cn_rare_kernel untouched, as in cn_kernel.
-// A/B on wimax_576_0.5 (tools/ab_cnrow.sh): 11.8 ms vs cn_kernel 14.2 ms;
-// W=4/K=48 (2 waves/SIMD), W=16/K=12, two-stage loads and persistent
-// workgroups were all slower.
+// Phase 1 issues its loads in S stages of K/S edges, so the workgroup fits in
+// 80 registers and three run per CU (latency hiding: the product chain parks
+// 7 of 8 wavefronts, phase 1 waits on HBM).  A/B on wimax_576_0.5
+// (tools/ab_cnrow.sh, profiles/r1f_cnrow_s4): 10.5 ms vs 11.3 ms for all
+// loads at once at 4 waves/SIMD and 14.2 ms for cn_kernel; 3 stages tie;
+// W=4/K=48, W=16/K=12, 8-waves/SIMD shapes (spills) and persistent
+// workgroups were slower.
 constexpr int kRowW = 8, kRowK = 24;
-template <bool kFirst, bool kStream>
-__global__ __launch_bounds__(64 * kRowW, 4) void cn_row_kernel(DevGraph g, DevState st, int it_parity,
-                                                               const int *__restrict__ col_idx,
-                                                               const int *__restrict__ row_ptr) {
+// S: phase-1 load stages (K/S edges' loads in flight per stage); WPS: min
+// wavefronts per SIMD (register cap 512/WPS).
+template <bool kFirst, bool kStream, int S, int WPS>
+__global__ __launch_bounds__(64 * kRowW, WPS) void cn_row_kernel(DevGraph g, DevState st, int it_parity,
+                                                                 const int *__restrict__ col_idx,
+                                                                 const int *__restrict__ row_ptr, AtanhCoef ac) {
     constexpr int W = kRowW, K = kRowK;
     __shared__ MathLds mlds;
     __shared__ double chain[kTile];  // running product handed from wavefront to wavefront
@@ -274,21 +280,26 @@ __global__ __launch_bounds__(64 * kRowW, 4) void cn_row_kernel(DevGraph g, DevSt
     const int c0 = beg + wave * C;
     const int cnt = max(0, min(end, c0 + C) - c0);  // wave-uniform, <= K (host checks deg <= W*K)
 
-    double t[K], eo[K];
+    double t[K];
     bool tiny = false;
     if (cnt > 0) {
 #pragma unroll
-        for (int i = 0; i < K; ++i) {
-            const int e = c0 + min(i, cnt - 1);
-            t[i] = Lt[col_idx[e] * kTile];
-            eo[i] = kFirst ? 0.0 : Et[e * kTile];
-        }
+        for (int h = 0; h < S; ++h) {
+            constexpr int H = K / S;
+            double eo[H];
 #pragma unroll
-        for (int i = 0; i < K; ++i) {
-            if (i < cnt) {
-                const double M = kFirst ? t[i] : t[i] - ((kStream && fresh) ? 0.0 : eo[i]);
-                t[i] = cn_tanh(M, ttab);
-                tiny |= !(fabs(t[i]) > kTiny);
+            for (int i = h * H; i < (h + 1) * H; ++i) {
+                const int e = c0 + min(i, cnt - 1);
+                t[i] = Lt[col_idx[e] * kTile];
+                eo[i - h * H] = kFirst ? 0.0 : Et[e * kTile];
+            }
+#pragma unroll
+            for (int i = h * H; i < (h + 1) * H; ++i) {
+                if (i < cnt) {
+                    const double M = kFirst ? t[i] : t[i] - ((kStream && fresh) ? 0.0 : eo[i - h * H]);
+                    t[i] = cn_tanh(M, ttab);
+                    tiny |= !(fabs(t[i]) > kTiny);
+                }
             }
         }
     }
@@ -316,7 +327,7 @@ __global__ __launch_bounds__(64 * kRowW, 4) void cn_row_kernel(DevGraph g, DevSt
 #ifdef LDPC_DIAG_NOMATH
             const double En = P * t[i];
 #else
-            const double En = 2.0 * atanh_f(clip_cl(P / t[i]), ltab);
+            const double En = 2.0 * atanh_f(clip_cl(P / t[i]), ltab, ac);
 #endif
             if (live) Et[(c0 + i) * kTile] = En;
         }
@@ -326,7 +337,7 @@ __global__ __launch_bounds__(64 * kRowW, 4) void cn_row_kernel(DevGraph g, DevSt
 // Rows recorded by cn_kernel: same update, with t parked in this wavefront's
 // own scratch slot (slot = global wavefront id; grid-stride over the list).
 template <bool kFirst, bool kStream>
-__global__ __launch_bounds__(256) void cn_rare_kernel(DevGraph g, DevState st, int it_parity) {
+__global__ __launch_bounds__(256) void cn_rare_kernel(DevGraph g, DevState st, int it_parity, AtanhCoef ac) {
     __shared__ MathLds mlds;
     const int count = st.rare_count[it_parity];
     if (blockIdx.x == 0 && threadIdx.x == 0) st.rare_count[it_parity ^ 1] = 0;  // for the next CN
@@ -371,7 +382,7 @@ __global__ __launch_bounds__(256) void cn_rare_kernel(DevGraph g, DevState st, i
                     first = false;
                 }
             }
-            const double En = 2.0 * atanh_f(clip_cl(q), ltab);
+            const double En = 2.0 * atanh_f(clip_cl(q), ltab, ac);
             if (live) Et[e * kTile] = En;
         }
     }
@@ -738,10 +749,24 @@ bool use_cn_row(const DevGraph &g) {
     return force != 0 && g.max_row_deg <= kRowW * kRowK;
 }
 
+// LDPC_CN_ROW_VARIANT=1 (A/B): all loads at once at 4 waves/SIMD (2 workgroups
+// per CU, 128 VGPRs) instead of 4 load stages at 6 waves/SIMD (3 per CU, 80).
+inline int cn_row_variant() {
+    static const int v = [] {
+        const char *e = getenv("LDPC_CN_ROW_VARIANT");
+        return e ? atoi(e) : 0;
+    }();
+    return v;
+}
+
 template <bool kFirst, bool kStream>
 void launch_cn_row(const DevGraph &g, const DevState &st, int par, hipStream_t s) {
     const unsigned grid = (unsigned)(((st.ntiles + 7) / 8) * 8 * g.m);
-    cn_row_kernel<kFirst, kStream><<<grid, 64 * kRowW, 0, s>>>(g, st, par, g.col_idx, g.row_ptr);
+    const int *ci = g.col_idx, *rp = g.row_ptr;
+    if (cn_row_variant() == 1)
+        cn_row_kernel<kFirst, kStream, 1, 4><<<grid, 64 * kRowW, 0, s>>>(g, st, par, ci, rp, kAtanhCoef);
+    else
+        cn_row_kernel<kFirst, kStream, 4, 6><<<grid, 64 * kRowW, 0, s>>>(g, st, par, ci, rp, kAtanhCoef);
 }
 
 hipError_t launch_cn(const DevGraph &g, const DevState &st, int it, hipStream_t s, bool stream) {
@@ -759,11 +784,11 @@ hipError_t launch_cn(const DevGraph &g, const DevState &st, int it, hipStream_t 
     const unsigned grid = (unsigned)(((st.ntiles + 7) / 8) * 8 * bpt);
     const int par = it & 1;
     if (stream)
-        cn_kernel<false, true><<<grid, 256, cn_lds_pad(), s>>>(g, st, bpt, par, g.col_idx, g.row_ptr);
+        cn_kernel<false, true><<<grid, 256, cn_lds_pad(), s>>>(g, st, bpt, par, g.col_idx, g.row_ptr, kAtanhCoef);
     else if (it == 0)
-        cn_kernel<true, false><<<grid, 256, cn_lds_pad(), s>>>(g, st, bpt, par, g.col_idx, g.row_ptr);
+        cn_kernel<true, false><<<grid, 256, cn_lds_pad(), s>>>(g, st, bpt, par, g.col_idx, g.row_ptr, kAtanhCoef);
     else
-        cn_kernel<false, false><<<grid, 256, cn_lds_pad(), s>>>(g, st, bpt, par, g.col_idx, g.row_ptr);
+        cn_kernel<false, false><<<grid, 256, cn_lds_pad(), s>>>(g, st, bpt, par, g.col_idx, g.row_ptr, kAtanhCoef);
     return hipGetLastError();
 }
 
@@ -771,11 +796,11 @@ hipError_t launch_cn_rare(const DevGraph &g, const DevState &st, int it, hipStre
     const unsigned grid = (unsigned)(st.nslots / 4);
     const int par = it & 1;
     if (stream)
-        cn_rare_kernel<false, true><<<grid, 256, 0, s>>>(g, st, par);
+        cn_rare_kernel<false, true><<<grid, 256, 0, s>>>(g, st, par, kAtanhCoef);
     else if (it == 0)
-        cn_rare_kernel<true, false><<<grid, 256, 0, s>>>(g, st, par);
+        cn_rare_kernel<true, false><<<grid, 256, 0, s>>>(g, st, par, kAtanhCoef);
     else
-        cn_rare_kernel<false, false><<<grid, 256, 0, s>>>(g, st, par);
+        cn_rare_kernel<false, false><<<grid, 256, 0, s>>>(g, st, par, kAtanhCoef);
     return hipGetLastError();
 }
 

@@ -67,10 +67,25 @@ struct LogEntry {
     double invc, hi, lo;
 };
 
+// Polynomial coefficients of log_hilo / atanh_f.  Kernels take a copy as a
+// kernel argument: the values then live in SGPRs and feed v_fma_f64 directly
+// (gfx950 VOP3 has no 64-bit literals, so literal coefficients are copied into
+// VGPRs before every use -- two v_mov each, per edge).  Same values either way.
+struct AtanhCoef {
+    double t13, t11, t9, t7, t5, t3;      // atanh Taylor: 1/13 .. 1/3
+    double l8, l7, l6, l5, l4, l3, l2;    // log1p(r) - r: -1/8, 1/7, -1/6, 1/5, -1/4, 1/3, -1/2
+    double ln2hi, ln2lo;
+};
+constexpr AtanhCoef kAtanhCoef{1.0 / 13.0, 1.0 / 11.0, 1.0 / 9.0, 1.0 / 7.0, 0.2, 1.0 / 3.0,
+                               -0.125, 0x1.2492492492492p-3, -0x1.5555555555555p-3, 0x1.999999999999ap-3,
+                               -0.25, 0x1.5555555555555p-2, -0.5,
+                               kLn2Hi, kLn2Lo};
+
 // log(x) = hi + lo for a positive normal x.  Accurate away from x ~ 1 (the
 // interval holding 1.0 itself is exact: invc = 1), which is all atanh needs.
 template <class LogTab>
-__host__ __device__ __forceinline__ void log_hilo(double x, const LogTab &lt, double &hi, double &lo) {
+__host__ __device__ __forceinline__ void log_hilo(double x, const LogTab &lt, double &hi, double &lo,
+                                                  const AtanhCoef &c = kAtanhCoef) {
     // glibc-style reduction on the high word only (the offset's low word is 0,
     // so no borrow): tmp = hi(x) - hi(OFF); 32-bit integer ops throughout.
     const uint64_t ix = dbits(x);
@@ -81,17 +96,17 @@ __host__ __device__ __forceinline__ void log_hilo(double x, const LogTab &lt, do
     const LogEntry t = lt(i);
     const double r = __builtin_fma(z, t.invc, -1.0);  // |r| < 2^-7
     const double kd = (double)k;
-    const double w = __builtin_fma(kd, kLn2Hi, t.hi);  // exact
+    const double w = __builtin_fma(kd, c.ln2hi, t.hi);  // exact
     hi = w + r;
     const double r2 = r * r;
     // log1p(r) - r, Taylor to r^8
-    double p = __builtin_fma(r, -0.125, 0x1.2492492492492p-3);   // -1/8, 1/7
-    p = __builtin_fma(p, r, -0x1.5555555555555p-3);               // -1/6
-    p = __builtin_fma(p, r, 0x1.999999999999ap-3);                // 1/5
-    p = __builtin_fma(p, r, -0.25);                               // -1/4
-    p = __builtin_fma(p, r, 0x1.5555555555555p-2);                // 1/3
-    p = __builtin_fma(p, r, -0.5);                                // -1/2
-    lo = ((w - hi) + r) + (__builtin_fma(kd, kLn2Lo, t.lo) + r2 * p);
+    double p = __builtin_fma(r, c.l8, c.l7);  // -1/8, 1/7
+    p = __builtin_fma(p, r, c.l6);            // -1/6
+    p = __builtin_fma(p, r, c.l5);            // 1/5
+    p = __builtin_fma(p, r, c.l4);            // -1/4
+    p = __builtin_fma(p, r, c.l3);            // 1/3
+    p = __builtin_fma(p, r, c.l2);            // -1/2
+    lo = ((w - hi) + r) + (__builtin_fma(kd, c.ln2lo, t.lo) + r2 * p);
 }
 
 // ~1-ulp reciprocal (v_rcp_f64); only used where the result is corrected or
@@ -106,16 +121,16 @@ __host__ __device__ __forceinline__ double fast_rcp(double d) {
 
 // atanh(q) for |q| <= CL.
 template <class LogTab>
-__host__ __device__ __forceinline__ double atanh_f(double q, const LogTab &lt) {
+__host__ __device__ __forceinline__ double atanh_f(double q, const LogTab &lt, const AtanhCoef &c = kAtanhCoef) {
     const double a = __builtin_fabs(q);
     double res;
     if (a < 0x1p-5) {
         const double a2 = a * a;
-        double p = __builtin_fma(a2, 1.0 / 13.0, 1.0 / 11.0);
-        p = __builtin_fma(p, a2, 1.0 / 9.0);
-        p = __builtin_fma(p, a2, 1.0 / 7.0);
-        p = __builtin_fma(p, a2, 0.2);
-        p = __builtin_fma(p, a2, 1.0 / 3.0);
+        double p = __builtin_fma(a2, c.t13, c.t11);
+        p = __builtin_fma(p, a2, c.t9);
+        p = __builtin_fma(p, a2, c.t7);
+        p = __builtin_fma(p, a2, c.t5);
+        p = __builtin_fma(p, a2, c.t3);
         res = __builtin_fma(a * a2, p, a);
     } else {
         // atanh(a) = log(y)/2, y = (1+a)/(1-a) carried as y_hi + y_lo:
@@ -131,7 +146,7 @@ __host__ __device__ __forceinline__ double atanh_f(double q, const LogTab &lt) {
         const double rem = __builtin_fma(-yh, v, u);
         const double corr = __builtin_fma(-yh, cv, rem + cu) * fast_rcp(u);
         double h, l;
-        log_hilo(yh, lt, h, l);
+        log_hilo(yh, lt, h, l, c);
         res = 0.5 * (h + (l + corr));
     }
     return dfrom(dbits(res) | (dbits(q) & 0x8000000000000000ull));
