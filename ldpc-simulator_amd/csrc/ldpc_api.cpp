@@ -740,7 +740,8 @@ int phys_grid(const DevGraph &G) {
         if (hipGetDeviceProperties(&p, dev) == hipSuccess && p.multiProcessorCount > 0) cus = p.multiProcessorCount;
     }
     const size_t lds = ldpc::phys_lds_bytes(G) + 64;
-    int per_cu = (int)std::min<size_t>(8, kLdsLimit / lds);  // <= 32 waves / CU at 4 waves per block
+    const int waves = ldpc::phys_block_threads(G) / 64;  // <= 32 waves / CU
+    int per_cu = (int)std::min<size_t>(32 / waves, kLdsLimit / lds);
     if (per_cu < 1) per_cu = 1;
     return cus * per_cu;
 }

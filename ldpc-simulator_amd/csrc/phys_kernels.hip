@@ -22,6 +22,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <cstdlib>
 
 #include "phys_math.h"
 #include "spa_device.h"
@@ -44,6 +45,62 @@ struct PhysArgs {
     unsigned long long *ctr;  // MC: counters [7] or null
 };
 
+// Frame f into LDS: Lambda = -channel LLR, L = Lambda, E = 0.
+__device__ __forceinline__ void frame_load(const PhysArgs &a, int f, float *E, float *L, float *Lam, int tid,
+                                           int nt) {
+    const DevGraph &g = a.g;
+    for (int j = tid; j < g.n; j += nt) {
+        const double ch = a.layout == 0 ? a.llr[(size_t)f * g.n + j]
+                                        : a.llr[((size_t)(f >> 6) * g.n + j) * kTile + (f & 63)];
+        Lam[j] = -(float)ch;
+        L[j] = Lam[j];
+    }
+    for (int e = tid; e < g.nnz; e += nt) E[e] = 0.0f;
+}
+
+// Outputs and Monte-Carlo counters of frame f (conv = -1: not converged).
+__device__ __forceinline__ void frame_finish(const PhysArgs &a, int f, int conv, const float *L, int *s_err,
+                                             int tid, int nt) {
+    const DevGraph &g = a.g;
+    const int iters = conv >= 0 ? conv + 1 : a.max_iter;
+    for (int j = tid; j < g.n; j += nt) {
+        const bool bit = L[j] < 0.0f;
+        if (a.z_out) a.z_out[(size_t)f * g.n + j] = bit ? 0 : 1;
+        if (a.post_out) a.post_out[(size_t)f * g.n + j] = L[j];
+    }
+    if (tid == 0) {
+        if (a.conv_out) a.conv_out[f] = conv;
+        if (a.status_out) a.status_out[f] = conv >= 0 ? 0 : 1;
+        if (a.iters_out) a.iters_out[f] = iters;
+        *s_err = 0;
+    }
+    if (a.ctr) {
+        __syncthreads();
+        if (conv < 0) {  // BER counts failed frames only (main.py:130-138)
+            const int kw = (g.k + 31) >> 5;
+            int my = 0;
+            for (int j = tid; j < g.k; j += nt) {
+                const uint32_t w = a.ubits[((size_t)(f >> 6) * kw + (j >> 5)) * kTile + (f & 63)];
+                my += (((w >> (j & 31)) & 1u) != (L[j] < 0.0f ? 1u : 0u)) ? 1 : 0;
+            }
+            atomicAdd(s_err, my);
+        }
+        __syncthreads();
+        if (tid == 0) {
+            atomicAdd(&a.ctr[0], 1ull);
+            if (conv < 0) {
+                atomicAdd(&a.ctr[1], 1ull);
+                atomicAdd(&a.ctr[2], (unsigned long long)*s_err);
+            } else {
+                atomicAdd(&a.ctr[3], (unsigned long long)conv);
+                atomicAdd(&a.ctr[4], 1ull);
+            }
+            atomicAdd(&a.ctr[6], (unsigned long long)iters);
+        }
+    }
+    __syncthreads();  // LDS reused by the next frame
+}
+
 __global__ __launch_bounds__(256) void phys_kernel(PhysArgs a) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     const DevGraph &g = a.g;
@@ -53,14 +110,7 @@ __global__ __launch_bounds__(256) void phys_kernel(PhysArgs a) {
     __shared__ int s_err;
     const int tid = threadIdx.x, nt = blockDim.x;
     for (int f = blockIdx.x; f < a.count; f += gridDim.x) {
-        // --- load the frame: Lambda = -channel LLR
-        for (int j = tid; j < g.n; j += nt) {
-            const double ch = a.layout == 0 ? a.llr[(size_t)f * g.n + j]
-                                            : a.llr[((size_t)(f >> 6) * g.n + j) * kTile + (f & 63)];
-            Lam[j] = -(float)ch;
-            L[j] = Lam[j];
-        }
-        for (int e = tid; e < g.nnz; e += nt) E[e] = 0.0f;
+        frame_load(a, f, E, L, Lam, tid, nt);
         __syncthreads();
         int conv = -1, it = 0;
         for (; it < a.max_iter; ++it) {
@@ -100,44 +150,115 @@ __global__ __launch_bounds__(256) void phys_kernel(PhysArgs a) {
                 break;
             }
         }
-        const int iters = conv >= 0 ? conv + 1 : a.max_iter;
-        // --- outputs
-        for (int j = tid; j < g.n; j += nt) {
-            const bool bit = L[j] < 0.0f;
-            if (a.z_out) a.z_out[(size_t)f * g.n + j] = bit ? 0 : 1;
-            if (a.post_out) a.post_out[(size_t)f * g.n + j] = L[j];
+        frame_finish(a, f, conv, L, &s_err, tid, nt);
+    }
+}
+
+// The same decoder with every thread's rows and columns fixed for the whole
+// launch (row r = tid + k*NT, column j = tid + k*NT), their column indices and
+// CSC edge ids held in registers as 16-bit pairs (loaded once, reused for every
+// frame: no index loads in the iteration loop), and phi(|M|) kept in registers
+// between the two sweeps of a row (phys_cn_tile does the same).  Identical
+// operations in identical order as phys_kernel: bit-identical results.
+template <int NT, int RPT, int RDEG, int CPT, int CDEG, int WPS>
+__global__ __launch_bounds__(NT, WPS) void phys_reg_kernel(PhysArgs a) {
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+    const DevGraph &g = a.g;
+    float *E = lds;
+    float *L = E + ((g.nnz + 3) & ~3);
+    float *Lam = L + ((g.n + 3) & ~3);
+    __shared__ int s_err;
+    const int tid = threadIdx.x;
+    int rbeg[RPT], rdeg[RPT];
+    uint32_t rc[RPT][RDEG / 2];
+#pragma unroll
+    for (int k = 0; k < RPT; ++k) {
+        const int r = tid + k * NT;
+        rbeg[k] = r < g.m ? g.row_ptr[r] : 0;
+        rdeg[k] = r < g.m ? g.row_ptr[r + 1] - rbeg[k] : 0;
+#pragma unroll
+        for (int i = 0; i < RDEG / 2; ++i) {
+            const uint32_t lo = 2 * i < rdeg[k] ? (uint32_t)g.col_idx[rbeg[k] + 2 * i] : 0u;
+            const uint32_t hi = 2 * i + 1 < rdeg[k] ? (uint32_t)g.col_idx[rbeg[k] + 2 * i + 1] : 0u;
+            rc[k][i] = lo | (hi << 16);
         }
-        if (tid == 0) {
-            if (a.conv_out) a.conv_out[f] = conv;
-            if (a.status_out) a.status_out[f] = conv >= 0 ? 0 : 1;
-            if (a.iters_out) a.iters_out[f] = iters;
-            s_err = 0;
+    }
+    int cdeg[CPT];
+    uint32_t ce[CPT][CDEG / 2];
+#pragma unroll
+    for (int k = 0; k < CPT; ++k) {
+        const int j = tid + k * NT;
+        const int p0 = j < g.n ? g.csc_ptr[j] : 0;
+        cdeg[k] = j < g.n ? g.csc_ptr[j + 1] - p0 : 0;
+#pragma unroll
+        for (int i = 0; i < CDEG / 2; ++i) {
+            const uint32_t lo = 2 * i < cdeg[k] ? (uint32_t)g.csc_edge[p0 + 2 * i] : 0u;
+            const uint32_t hi = 2 * i + 1 < cdeg[k] ? (uint32_t)g.csc_edge[p0 + 2 * i + 1] : 0u;
+            ce[k][i] = lo | (hi << 16);
         }
-        if (a.ctr) {
-            __syncthreads();
-            if (conv < 0) {  // BER counts failed frames only (main.py:130-138)
-                const int kw = (g.k + 31) >> 5;
-                int my = 0;
-                for (int j = tid; j < g.k; j += nt) {
-                    const uint32_t w = a.ubits[((size_t)(f >> 6) * kw + (j >> 5)) * kTile + (f & 63)];
-                    my += (((w >> (j & 31)) & 1u) != (L[j] < 0.0f ? 1u : 0u)) ? 1 : 0;
+    }
+    auto col = [&](int k, int i) -> int { return (int)((rc[k][i >> 1] >> ((i & 1) * 16)) & 0xffffu); };
+    auto edge = [&](int k, int i) -> int { return (int)((ce[k][i >> 1] >> ((i & 1) * 16)) & 0xffffu); };
+
+    for (int f = blockIdx.x; f < a.count; f += gridDim.x) {
+        frame_load(a, f, E, L, Lam, tid, NT);
+        __syncthreads();
+        int conv = -1;
+        for (int it = 0; it < a.max_iter; ++it) {
+            // --- check nodes
+#pragma unroll
+            for (int k = 0; k < RPT; ++k) {
+                if (rdeg[k] == 0) continue;
+                float ph[RDEG];
+                uint32_t sg = 0u;
+                float S = 0.0f;
+#pragma unroll
+                for (int i = 0; i < RDEG; ++i) {
+                    if (i < rdeg[k]) {
+                        const float M = L[col(k, i)] - E[rbeg[k] + i];
+                        ph[i] = phi(fabsf(M));
+                        S += ph[i];
+                        sg |= (M < 0.0f ? 1u : 0u) << i;
+                    }
                 }
-                atomicAdd(&s_err, my);
+                const uint32_t neg = __popc(sg) & 1u;
+#pragma unroll
+                for (int i = 0; i < RDEG; ++i) {
+                    if (i < rdeg[k]) {
+                        const float mag = phi(fmaxf(S - ph[i], 0.0f));
+                        E[rbeg[k] + i] = ((neg ^ (sg >> i)) & 1u) ? -mag : mag;
+                    }
+                }
             }
             __syncthreads();
-            if (tid == 0) {
-                atomicAdd(&a.ctr[0], 1ull);
-                if (conv < 0) {
-                    atomicAdd(&a.ctr[1], 1ull);
-                    atomicAdd(&a.ctr[2], (unsigned long long)s_err);
-                } else {
-                    atomicAdd(&a.ctr[3], (unsigned long long)conv);
-                    atomicAdd(&a.ctr[4], 1ull);
-                }
-                atomicAdd(&a.ctr[6], (unsigned long long)iters);
+            // --- variable nodes
+#pragma unroll
+            for (int k = 0; k < CPT; ++k) {
+                const int j = tid + k * NT;
+                if (j >= g.n) continue;
+                float s = Lam[j];
+#pragma unroll
+                for (int i = 0; i < CDEG; ++i)
+                    if (i < cdeg[k]) s += E[edge(k, i)];
+                L[j] = s;
+            }
+            __syncthreads();
+            // --- syndrome of b = (L < 0)
+            uint32_t bad = 0u;
+#pragma unroll
+            for (int k = 0; k < RPT; ++k) {
+                uint32_t par = 0u;
+#pragma unroll
+                for (int i = 0; i < RDEG; ++i)
+                    if (i < rdeg[k]) par ^= (L[col(k, i)] < 0.0f) ? 1u : 0u;
+                bad |= par;
+            }
+            if (!__syncthreads_or((int)bad)) {
+                conv = it;
+                break;
             }
         }
-        __syncthreads();  // LDS reused by the next frame
+        frame_finish(a, f, conv, L, &s_err, tid, NT);
     }
 }
 
@@ -147,12 +268,69 @@ size_t phys_lds_bytes(const DevGraph &g) {
     return sizeof(float) * (size_t)(((g.nnz + 3) & ~3) + 2 * ((g.n + 3) & ~3));
 }
 
+namespace {
+
+// Shape of phys_reg_kernel for this graph (0 = none: the generic phys_kernel).
+// LDPC_PHYS_REG=0 forces phys_kernel (A/B).
+struct RegShape {
+    int rpt, rdeg, cpt, cdeg;
+};
+constexpr int kRegNT = 512;
+constexpr RegShape kRegShapes[] = {{1, 8, 1, 8}, {1, 8, 2, 8}, {2, 8, 3, 8}, {2, 16, 5, 8}, {3, 8, 5, 8}};
+
+int reg_shape(const DevGraph &g) {
+    static const int force = [] {
+        const char *e = getenv("LDPC_PHYS_REG");
+        return e ? atoi(e) : -1;
+    }();
+    if (force == 0 || g.nnz >= 65536 || g.n >= 65536) return -1;  // 16-bit indices
+    const int mc = g.max_col_deg;
+    const int rpt = (g.m + kRegNT - 1) / kRegNT, cpt = (g.n + kRegNT - 1) / kRegNT;
+    int best = -1;
+    for (int i = 0; i < (int)(sizeof(kRegShapes) / sizeof(kRegShapes[0])); ++i) {
+        const RegShape &r = kRegShapes[i];
+        if (r.rpt >= rpt && r.cpt >= cpt && r.rdeg >= g.max_row_deg && r.cdeg >= mc &&
+            (best < 0 || r.rpt * r.rdeg + r.cpt * r.cdeg <
+                             kRegShapes[best].rpt * kRegShapes[best].rdeg + kRegShapes[best].cpt * kRegShapes[best].cdeg))
+            best = i;
+    }
+    return best;
+}
+
+}  // namespace
+
+int phys_block_threads(const DevGraph &g) { return reg_shape(g) >= 0 ? kRegNT : 256; }
+
 hipError_t launch_phys(const DevGraph &g, const double *llr, int layout, int count, int max_iter, uint8_t *z,
                        int *conv, int *status, int *iters, float *post, const uint32_t *ubits,
                        unsigned long long *ctr, int grid, hipStream_t s) {
     PhysArgs a{g, llr, layout, count, max_iter, z, conv, status, iters, post, ubits, ctr};
     const size_t lds = phys_lds_bytes(g);
-    if (count > 0) phys_kernel<<<grid, 256, lds, s>>>(a);
+    if (count <= 0) return hipSuccess;
+    // min waves per SIMD of the large shapes: 6 = three 8-wave frames per CU (the
+    // LDS limit for the 2304 codes) with a few spills beat 4 = two frames without
+    // (tools/ab_physreg.sh: 2304 r1/2 -2.5 dB 51.9 vs 59.2 ms); LDPC_PHYS_REG_WPS=4 (A/B)
+    static const int wps = [] {
+        const char *e = getenv("LDPC_PHYS_REG_WPS");
+        return e ? atoi(e) : 6;
+    }();
+    switch (reg_shape(g)) {
+    case 0: phys_reg_kernel<kRegNT, 1, 8, 1, 8, 6><<<grid, kRegNT, lds, s>>>(a); break;
+    case 1: phys_reg_kernel<kRegNT, 1, 8, 2, 8, 6><<<grid, kRegNT, lds, s>>>(a); break;
+    case 2:
+        if (wps == 6) phys_reg_kernel<kRegNT, 2, 8, 3, 8, 6><<<grid, kRegNT, lds, s>>>(a);
+        else phys_reg_kernel<kRegNT, 2, 8, 3, 8, 4><<<grid, kRegNT, lds, s>>>(a);
+        break;
+    case 3:
+        if (wps == 6) phys_reg_kernel<kRegNT, 2, 16, 5, 8, 6><<<grid, kRegNT, lds, s>>>(a);
+        else phys_reg_kernel<kRegNT, 2, 16, 5, 8, 4><<<grid, kRegNT, lds, s>>>(a);
+        break;
+    case 4:
+        if (wps == 6) phys_reg_kernel<kRegNT, 3, 8, 5, 8, 6><<<grid, kRegNT, lds, s>>>(a);
+        else phys_reg_kernel<kRegNT, 3, 8, 5, 8, 4><<<grid, kRegNT, lds, s>>>(a);
+        break;
+    default: phys_kernel<<<grid, 256, lds, s>>>(a);
+    }
     return hipGetLastError();
 }
 

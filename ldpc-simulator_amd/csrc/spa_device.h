@@ -83,6 +83,7 @@ hipError_t launch_count(const DevGraph &g, const DevState &st, unsigned long lon
 
 // physical mode (phys_kernels.hip)
 size_t phys_lds_bytes(const DevGraph &g);
+int phys_block_threads(const DevGraph &g);  // threads per workgroup launch_phys uses
 hipError_t launch_phys(const DevGraph &g, const double *llr, int layout, int count, int max_iter, uint8_t *z,
                        int *conv, int *status, int *iters, float *post, const uint32_t *ubits,
                        unsigned long long *ctr, int grid, hipStream_t s);
