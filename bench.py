@@ -332,7 +332,9 @@ def main():
                                       "phys_cn_ms": cms, "phys_vn_ms": vms, "gen_ms": prof["generate"][0],
                                       "count_ms": prof["count"][0]}
         else:
-            out["roofline"] = {"bound": "valu", "kernel": "phys_kernel", "launches": pl,
+            from ldpc_amd import _lib
+            pname = _lib.lib().ldpc_phys_kernel_name(pgraph.handle, 0).decode()
+            out["roofline"] = {"bound": "valu", "kernel": pname, "launches": pl,
                                "avg_launch_ms": pms / max(pl, 1),
                                "note": "state in LDS; HBM traffic is the frame input only"}
             out["decode_roofline"] = {"phys_ms": pms, "gen_ms": prof["generate"][0]}

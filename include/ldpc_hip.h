@@ -87,6 +87,9 @@ int ldpc_graph_destroy(ldpc_graph *g);
  * ("cn_row_kernel": rows of degree <= 192 kept in registers, 16 B/edge;
  * "cn_kernel": one wavefront per row, 24 B/edge) -- measurement labels. */
 const char *ldpc_cn_kernel_name(const ldpc_graph *g);
+/* Physical-mode kernel for this (sparse) graph: "phys_reg_kernel" / "phys_kernel"
+ * (state in LDS) or "phys_cn_tile_kernel" (state in HBM). */
+const char *ldpc_phys_kernel_name(const ldpc_graph *g, uint32_t flags);
 int ldpc_graph_info(const ldpc_graph *g, int32_t *m, int32_t *n, int64_t *nnz,
                     int32_t *max_row_deg, int32_t *max_col_deg);
 

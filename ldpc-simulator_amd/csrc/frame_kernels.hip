@@ -106,8 +106,8 @@ __global__ __launch_bounds__(64) void ira_carry_kernel(DevGraph g, PhysTile pt) 
     }
 }
 
-// to_lambda: write the decoder's fp32 Lambda = L = -llr directly (physical
-// Monte-Carlo), else the fp64 channel LLRs ch (ldpc_generate_frames).
+// to_lambda: write the tile decoder's fp32 Lambda = L = -llr directly
+// (kFramesTileLambda), else the fp64 channel LLRs ch (kFramesCh).
 __global__ __launch_bounds__(64) void frame_channel_kernel(DevGraph g, DevState st, PhysTile pt, uint64_t seed,
                                                          int snr_point, double sigma, int64_t frame0,
                                                          int to_lambda) {
@@ -153,7 +153,43 @@ __global__ __launch_bounds__(64) void frame_channel_kernel(DevGraph g, DevState 
 }
 
 
+// The same draws written row-major, Lambda = -llr as fp32 [count][n] (the LDS
+// physical decoder reads a frame contiguously): one wavefront per (frame, 64
+// column pairs), lane = column pair.
+__global__ __launch_bounds__(64) void frame_channel_row_kernel(DevGraph g, DevState st, PhysTile pt, uint64_t seed,
+                                                             int snr_point, double sigma, int64_t frame0,
+                                                             float *__restrict__ row_out) {
+    const int kw = (g.k + 31) >> 5;
+    const int mw = (g.m + 31) >> 5;
+    const int mw32 = (mw + 31) >> 5;
+    const int npairs = (g.n + 1) >> 1;
+    const int per_frame = (npairs + 63) >> 6;
+    const int f = blockIdx.x / per_frame;
+    const int b = (blockIdx.x % per_frame) * 64 + threadIdx.x;
+    if (f >= st.count || b >= npairs) return;
+    const int tile = f >> 6, lf = f & 63;
+    const double s2 = sigma * sigma;
+    const uint32_t *Ut = st.ubits + (size_t)tile * kw * kTile + lf;
+    const uint32_t *Pt = pt.pbits + (size_t)tile * mw * kTile + lf;
+    const uint32_t *Wt = pt.wpar + (size_t)tile * mw32 * kTile + lf;
+    double gz[2];
+    noise_pair(seed, frame0 + f, snr_point, b, gz);
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+        const int j = 2 * b + q;
+        if (j >= g.n) break;
+        const int r = j - g.k;
+        const int w = r >> 5;
+        const uint32_t bit = j < g.k ? (Ut[(j >> 5) * kTile] >> (j & 31)) & 1u
+                                     : ((Pt[w * kTile] >> (r & 31)) ^ (Wt[(w >> 5) * kTile] >> (w & 31))) & 1u;
+        row_out[(size_t)f * g.n + j] = -(float)channel_llr(bit, gz[q], s2);
+    }
+}
+
 // p_r = parity(A_r & u) for the 32 rows of one word; wpar stays zero (no carry).
+// KW > 0: the frame's u words are held in registers (kw <= KW) and A's words
+// come through scalar loads; KW = 0: any kw, u re-read per row.
+template <int KW>
 __global__ __launch_bounds__(256) void std_parity_kernel(DevGraph g, DevState st, PhysTile pt,
                                                          const uint32_t *__restrict__ apack) {
     const int kw = (g.k + 31) >> 5;
@@ -166,11 +202,25 @@ __global__ __launch_bounds__(256) void std_parity_kernel(DevGraph g, DevState st
     const uint32_t *Ut = st.ubits + (size_t)tile * kw * kTile + lane;
     uint32_t word = 0u;
     const int r1 = min(g.m, (w + 1) * 32);
-    for (int r = w * 32; r < r1; ++r) {
-        const uint32_t *ar = apack + (size_t)r * kw;
-        uint32_t acc = 0u;
-        for (int i = 0; i < kw; ++i) acc ^= ar[i] & Ut[i * kTile];
-        word |= ((uint32_t)__popc(acc) & 1u) << (r & 31);
+    if constexpr (KW > 0) {
+        uint32_t u[KW];
+#pragma unroll
+        for (int i = 0; i < KW; ++i) u[i] = i < kw ? Ut[i * kTile] : 0u;
+        for (int r = w * 32; r < r1; ++r) {
+            const uint32_t *ar = apack + (size_t)r * kw;
+            uint32_t acc = 0u;
+#pragma unroll
+            for (int i = 0; i < KW; ++i)
+                if (i < kw) acc ^= ar[i] & u[i];
+            word |= ((uint32_t)__popc(acc) & 1u) << (r & 31);
+        }
+    } else {
+        for (int r = w * 32; r < r1; ++r) {
+            const uint32_t *ar = apack + (size_t)r * kw;
+            uint32_t acc = 0u;
+            for (int i = 0; i < kw; ++i) acc ^= ar[i] & Ut[i * kTile];
+            word |= ((uint32_t)__popc(acc) & 1u) << (r & 31);
+        }
     }
     pt.pbits[((size_t)tile * mw + w) * kTile + lane] = word;
 }
@@ -178,7 +228,7 @@ __global__ __launch_bounds__(256) void std_parity_kernel(DevGraph g, DevState st
 }  // namespace
 
 hipError_t launch_frames(const DevGraph &g, const DevState &st, const PhysTile &pt, uint64_t seed, int snr_point,
-                         double sigma, int64_t frame0, bool to_lambda, hipStream_t s) {
+                         double sigma, int64_t frame0, FramesOut out, float *row_out, hipStream_t s) {
     const int kw = (g.k + 31) >> 5, mw = (g.m + 31) >> 5;
     const int nblk = (kw + 3) >> 2, bpb = 16;
     const int nbc = (nblk + bpb - 1) / bpb;
@@ -190,11 +240,21 @@ hipError_t launch_frames(const DevGraph &g, const DevState &st, const PhysTile &
         ira_sbits_kernel<<<st.ntiles * ((mw + 3) >> 2), 256, 0, s>>>(g, st, pt, g.row_ptr, g.col_idx);
         ira_carry_kernel<<<st.ntiles, 64, 0, s>>>(g, pt);
     } else {
-        std_parity_kernel<<<st.ntiles * ((mw + 3) >> 2), 256, 0, s>>>(g, st, pt, g.a_packed);
+        const unsigned grid = (unsigned)(st.ntiles * ((mw + 3) >> 2));
+        if (kw <= 16)
+            std_parity_kernel<16><<<grid, 256, 0, s>>>(g, st, pt, g.a_packed);
+        else if (kw <= 64)
+            std_parity_kernel<64><<<grid, 256, 0, s>>>(g, st, pt, g.a_packed);
+        else
+            std_parity_kernel<0><<<grid, 256, 0, s>>>(g, st, pt, g.a_packed);
     }
     const int npairs = (g.n + 1) >> 1;
-    frame_channel_kernel<<<st.ntiles * ((npairs + 63) >> 6), 64, 0, s>>>(g, st, pt, seed, snr_point, sigma, frame0,
-                                                                       to_lambda ? 1 : 0);
+    if (out == kFramesRowLambda)
+        frame_channel_row_kernel<<<st.count * ((npairs + 63) >> 6), 64, 0, s>>>(g, st, pt, seed, snr_point, sigma,
+                                                                              frame0, row_out);
+    else
+        frame_channel_kernel<<<st.ntiles * ((npairs + 63) >> 6), 64, 0, s>>>(
+            g, st, pt, seed, snr_point, sigma, frame0, out == kFramesTileLambda ? 1 : 0);
     return hipGetLastError();
 }
 

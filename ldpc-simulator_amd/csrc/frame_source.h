@@ -36,9 +36,11 @@ __device__ __forceinline__ void noise_pair(uint64_t seed, int64_t F, int snr_poi
     const double u1 = u52(c[0], c[1]);
     const double u2 = u52(c[2], c[3]);
     const double r = sqrt(-2.0 * log(u1));
-    const double th = 6.283185307179586 * u2;
+    // cos/sin(2 pi u2) as sincospi(2 u2): no Payne-Hanek reduction; 2 u2 is
+    // exact, and the result differs from sin/cos(fl(2 pi u2)) (the CPU
+    // restatement) by ~1e-16 relative
     double sn, cs;
-    sincos(th, &sn, &cs);
+    sincospi(2.0 * u2, &sn, &cs);
     g[0] = r * cs;
     g[1] = r * sn;
 }

@@ -378,6 +378,16 @@ const char *ldpc_cn_kernel_name(const ldpc_graph *g) {
     return ldpc::use_cn_row(g->dg) ? "cn_row_kernel" : "cn_kernel";
 }
 
+namespace {
+bool phys_use_lds(const DevGraph &P, uint32_t flags);
+}
+
+const char *ldpc_phys_kernel_name(const ldpc_graph *g, uint32_t flags) {
+    if (!g) return "";
+    if (!phys_use_lds(g->dg, flags)) return "phys_cn_tile_kernel";
+    return ldpc::phys_block_threads(g->dg) > 256 ? "phys_reg_kernel" : "phys_kernel";
+}
+
 int ldpc_graph_info(const ldpc_graph *g, int32_t *m, int32_t *n, int64_t *nnz, int32_t *max_row_deg,
                     int32_t *max_col_deg) {
     if (!g) return ldpc_fail(LDPC_EINVAL, "ldpc_graph_info: NULL graph");
@@ -616,7 +626,8 @@ int ldpc_generate_frames(ldpc_decoder *d, uint64_t seed, int32_t snr_point, doub
         (void)hipFree(dev_ptrs ? nullptr : u_dev);
         return rc;
     }
-    HIP_TRY(ldpc::launch_frames(G, d->st, phys_tile(d), seed, snr_point, sigma, frame0, false, s));
+    HIP_TRY(ldpc::launch_frames(G, d->st, phys_tile(d), seed, snr_point, sigma, frame0, ldpc::kFramesCh, nullptr,
+                                s));
     // export writes u only for j<k, at [f][k]: give it the [count][k] buffer
     HIP_TRY(ldpc::launch_export_frames(G, d->st, u_dev, l_dev, s));
     if (!dev_ptrs) {
@@ -713,7 +724,7 @@ int ldpc_mc_run(ldpc_decoder *d, uint64_t seed, int32_t n_points, const double *
             const DevState st = d->st;
             HIP_TRY(timed(d, LDPC_K_GEN, s,
                           [&] { return ldpc::launch_frames(G, st, phys_tile(d), seed, p, sigmas[p], frame0 + start,
-                                                           false, s); }));
+                                                           ldpc::kFramesCh, nullptr, s); }));
             HIP_TRY(run_iterations(d, G, st, max_iter, nllr, s));
             HIP_TRY(timed(d, LDPC_K_COUNT, s, [&] {
                 return ldpc::launch_count(G, st, d->counters + (size_t)p * LDPC_MC_NCOUNT, s);
@@ -759,7 +770,7 @@ int phys_decode_lds(const ldpc_graph *g, int32_t batch, const double *llr, int32
     const DevGraph &G = g->dg;
     const size_t n = (size_t)G.n, B = (size_t)batch;
     if (flags & LDPC_F_DEVICE_PTRS) {
-        HIP_TRY(ldpc::launch_phys(G, llr, 0, batch, max_iter, z_out, conv_out, status_out, iters_out, post_out,
+        HIP_TRY(ldpc::launch_phys(G, llr, nullptr, 0, batch, max_iter, z_out, conv_out, status_out, iters_out, post_out,
                                   nullptr, nullptr, std::min(phys_grid(G), batch), s));
         return LDPC_OK;
     }
@@ -774,7 +785,7 @@ int phys_decode_lds(const ldpc_graph *g, int32_t batch, const double *llr, int32
     hipError_t e = hipSuccess;
     if (!rc) {
         e = hipMemcpyAsync(d_llr, llr, sizeof(double) * B * n, hipMemcpyHostToDevice, s);
-        if (!e) e = ldpc::launch_phys(G, d_llr, 0, batch, max_iter, d_z, d_i, d_i + B, d_i + 2 * B, d_post, nullptr,
+        if (!e) e = ldpc::launch_phys(G, d_llr, nullptr, 0, batch, max_iter, d_z, d_i, d_i + B, d_i + 2 * B, d_post, nullptr,
                                      nullptr, std::min(phys_grid(G), batch), s);
         if (!e && z_out) e = hipMemcpyAsync(z_out, d_z, B * n, hipMemcpyDeviceToHost, s);
         if (!e && conv_out) e = hipMemcpyAsync(conv_out, d_i, sizeof(int) * B, hipMemcpyDeviceToHost, s);
@@ -924,18 +935,20 @@ int ldpc_phys_mc_run(ldpc_decoder *d, const ldpc_graph *gp, uint64_t seed, int32
             const int cnt = (int)std::min<int64_t>(cap, frames_per_point - start);
             state_bind(d, (cnt + kTile - 1) / kTile, cnt);
             const DevState st = d->st;
-            // frames for the tile decoder go straight to its fp32 Lambda/L
-            const bool direct = !lds;
+            // frames go straight to the decoder's fp32 Lambda: tile layout for the
+            // HBM tile decoder, row-major (contiguous per frame) for the LDS decoder
+            float *rows = (float *)d->llr_stage;  // cap x n doubles: room for cap x n floats
             HIP_TRY(timed(d, LDPC_K_GEN, s, [&] {
-                return ldpc::launch_frames(G, st, phys_tile(d), seed, p, sigmas[p], frame0 + start, direct, s);
+                return ldpc::launch_frames(G, st, phys_tile(d), seed, p, sigmas[p], frame0 + start,
+                                           lds ? ldpc::kFramesRowLambda : ldpc::kFramesTileLambda, rows, s);
             }));
             if (lds) {
                 HIP_TRY(timed(d, LDPC_K_PHYS, s, [&] {
-                    return ldpc::launch_phys(P, st.ch, 1, cnt, max_iter, nullptr, nullptr, nullptr, nullptr, nullptr,
-                                             st.ubits, ctr, std::min(phys_grid(P), cnt), s);
+                    return ldpc::launch_phys(P, nullptr, rows, 2, cnt, max_iter, nullptr, nullptr, nullptr, nullptr,
+                                             nullptr, st.ubits, ctr, std::min(phys_grid(P), cnt), s);
                 }));
             } else {
-                if (int rc = phys_tile_decode(d, P, max_iter, !direct, s)) return rc;
+                if (int rc = phys_tile_decode(d, P, max_iter, false, s)) return rc;
                 HIP_TRY(timed(d, LDPC_K_COUNT, s,
                               [&] { return ldpc::launch_phys_tile_count(P, st, phys_tile(d), ctr, s); }));
             }

@@ -33,7 +33,8 @@ namespace {
 struct PhysArgs {
     DevGraph g;               // H[:, perm] (sparse)
     const double *llr;        // [count][n] (layout 0) or ch tile layout (layout 1)
-    int layout;               // 0: row per frame; 1: [tile][n][64] (on-device frames)
+    const float *lam;         // layout 2: [count][n] fp32 Lambda (on-device frames, frame_kernels.hip)
+    int layout;               // 0: row per frame; 1: [tile][n][64]; 2: lam
     int count;
     int max_iter;
     uint8_t *z_out;           // [count][n] or null: z = (bit estimate) ^ 1
@@ -50,9 +51,13 @@ __device__ __forceinline__ void frame_load(const PhysArgs &a, int f, float *E, f
                                            int nt) {
     const DevGraph &g = a.g;
     for (int j = tid; j < g.n; j += nt) {
-        const double ch = a.layout == 0 ? a.llr[(size_t)f * g.n + j]
-                                        : a.llr[((size_t)(f >> 6) * g.n + j) * kTile + (f & 63)];
-        Lam[j] = -(float)ch;
+        if (a.layout == 2) {
+            Lam[j] = a.lam[(size_t)f * g.n + j];  // contiguous per frame
+        } else {
+            const double ch = a.layout == 0 ? a.llr[(size_t)f * g.n + j]
+                                            : a.llr[((size_t)(f >> 6) * g.n + j) * kTile + (f & 63)];
+            Lam[j] = -(float)ch;
+        }
         L[j] = Lam[j];
     }
     for (int e = tid; e < g.nnz; e += nt) E[e] = 0.0f;
@@ -301,10 +306,10 @@ int reg_shape(const DevGraph &g) {
 
 int phys_block_threads(const DevGraph &g) { return reg_shape(g) >= 0 ? kRegNT : 256; }
 
-hipError_t launch_phys(const DevGraph &g, const double *llr, int layout, int count, int max_iter, uint8_t *z,
-                       int *conv, int *status, int *iters, float *post, const uint32_t *ubits,
+hipError_t launch_phys(const DevGraph &g, const double *llr, const float *lam, int layout, int count, int max_iter,
+                       uint8_t *z, int *conv, int *status, int *iters, float *post, const uint32_t *ubits,
                        unsigned long long *ctr, int grid, hipStream_t s) {
-    PhysArgs a{g, llr, layout, count, max_iter, z, conv, status, iters, post, ubits, ctr};
+    PhysArgs a{g, llr, lam, layout, count, max_iter, z, conv, status, iters, post, ubits, ctr};
     const size_t lds = phys_lds_bytes(g);
     if (count <= 0) return hipSuccess;
     // min waves per SIMD of the large shapes: 6 = three 8-wave frames per CU (the

@@ -84,16 +84,21 @@ hipError_t launch_count(const DevGraph &g, const DevState &st, unsigned long lon
 // physical mode (phys_kernels.hip)
 size_t phys_lds_bytes(const DevGraph &g);
 int phys_block_threads(const DevGraph &g);  // threads per workgroup launch_phys uses
-hipError_t launch_phys(const DevGraph &g, const double *llr, int layout, int count, int max_iter, uint8_t *z,
-                       int *conv, int *status, int *iters, float *post, const uint32_t *ubits,
+// layout 0: llr [count][n] fp64; 1: llr = ch tile layout; 2: lam [count][n] fp32 Lambda
+hipError_t launch_phys(const DevGraph &g, const double *llr, const float *lam, int layout, int count, int max_iter,
+                       uint8_t *z, int *conv, int *status, int *iters, float *post, const uint32_t *ubits,
                        unsigned long long *ctr, int grid, hipStream_t s);
 
 // physical mode, HBM-resident tiles + IRA frame source (phys_tile.hip)
 // on-device frames of a chunk (frame_kernels.hip): info bits -> st.ubits,
-// parities via pt.pbits/pt.wpar (H_std [A|I] or IRA graph), channel LLRs ->
-// st.ch (fp64), or with to_lambda the tile decoder's fp32 Lambda = L = -llr
+// parities via pt.pbits/pt.wpar (H_std [A|I] or IRA graph), channel LLRs as
+enum FramesOut {
+    kFramesCh = 0,          // st.ch, fp64 tile layout (parity decoder, export)
+    kFramesTileLambda = 1,  // pt.Lam and pt.L, fp32 tile layout (physical tile decoder)
+    kFramesRowLambda = 2,   // row_out [count][n] fp32 Lambda (physical LDS decoder)
+};
 hipError_t launch_frames(const DevGraph &g, const DevState &st, const PhysTile &pt, uint64_t seed, int snr_point,
-                         double sigma, int64_t frame0, bool to_lambda, hipStream_t s);
+                         double sigma, int64_t frame0, FramesOut out, float *row_out, hipStream_t s);
 // convert: L = Lambda = -(float)ch (else the generator already wrote them)
 hipError_t launch_phys_tile_init(const DevGraph &g, const DevState &st, const PhysTile &pt, bool convert,
                                  hipStream_t s);

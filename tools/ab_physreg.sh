@@ -9,7 +9,7 @@ run() {  # name, bench args..., env via ENVV
 import json; d=json.loads(open('gpurun_out/physreg/$name.log').read().strip().splitlines()[-1]); r=d['roofline']
 print('$name'.ljust(22), round(d['value']), 'cw/s  iters', round(d['avg_iters'],2), ' fer', round(d['fer'],4), ' phys', round(r['avg_launch_ms'],3), 'ms')"
 }
-for v in "generic:LDPC_PHYS_REG=0" "reg_w4:LDPC_PHYS_REG_WPS=4" "reg_w6:LDPC_PHYS_REG_WPS=6"; do
+for v in "reg:LDPC_PHYS_REG=1"; do
     tag=${v%%:*}; ENVV=${v#*:}
     run ${tag}_2304h_0 --code wimax_2304_0.5 --snr 0.0
     run ${tag}_2304h_-2.5 --code wimax_2304_0.5 --snr -2.5
