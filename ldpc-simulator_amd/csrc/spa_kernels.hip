@@ -95,15 +95,7 @@ __device__ __forceinline__ double cn_tanh(double M, const LdsTanh &t) {
 #ifdef LDPC_DIAG_NOMATH  // diagnostic build only: memory pattern without the math
     return d * 0.25 + 0.5;
 #endif
-#ifdef LDPC_BRANCHLESS_TANH
-    // evaluate tanh for every lane, then select: no exec-mask branches around
-    // the table lookups (the asm keeps the compiler from sinking it into one)
-    double r = np_tanh(d, t);
-    __asm__ volatile("" : "+v"(r));
-    return d > 17.5 ? kCL : (d < -17.5 ? -kCL : r);
-#else
     return d > 17.5 ? kCL : (d < -17.5 ? -kCL : np_tanh(d, t));
-#endif
 }
 
 // --------------------------------------------------------------- CN pass

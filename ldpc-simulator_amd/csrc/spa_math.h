@@ -124,32 +124,6 @@ template <class LogTab>
 __host__ __device__ __forceinline__ double atanh_f(double q, const LogTab &lt, const AtanhCoef &c = kAtanhCoef) {
     const double a = __builtin_fabs(q);
     double res;
-#if defined(LDPC_BRANCHLESS_ATANH) && defined(__HIP_DEVICE_COMPILE__)
-    {  // both paths for every lane, then select (no divergent branch)
-        const double a2 = a * a;
-        double p = __builtin_fma(a2, c.t13, c.t11);
-        p = __builtin_fma(p, a2, c.t9);
-        p = __builtin_fma(p, a2, c.t7);
-        p = __builtin_fma(p, a2, c.t5);
-        p = __builtin_fma(p, a2, c.t3);
-        double small = __builtin_fma(a * a2, p, a);
-        __asm__ volatile("" : "+v"(small));
-        const double u = 1.0 + a, v = 1.0 - a;
-        const double cu = a - (u - 1.0);
-        const double cv = -a - (v - 1.0);
-        const double rv = fast_rcp(v);
-        const double y0 = u * rv;
-        const double yh = __builtin_fma(__builtin_fma(-y0, v, u), rv, y0);
-        const double rem = __builtin_fma(-yh, v, u);
-        const double corr = __builtin_fma(-yh, cv, rem + cu) * fast_rcp(u);
-        double h, l;
-        log_hilo(yh, lt, h, l, c);
-        double big = 0.5 * (h + (l + corr));
-        __asm__ volatile("" : "+v"(big));
-        res = a < 0x1p-5 ? small : big;
-        return dfrom(dbits(res) | (dbits(q) & 0x8000000000000000ull));
-    }
-#endif
     if (a < 0x1p-5) {
         const double a2 = a * a;
         double p = __builtin_fma(a2, c.t13, c.t11);
