@@ -51,7 +51,10 @@ constexpr double kCL = 0.99999999999999878;  // spa_decoder.py:141,167
 constexpr double kTiny = 1e-10;              // spa_decoder.py:159
 constexpr int kCnRowsPerBlock = 4;           // 4 wavefronts = 4 rows of one tile
 constexpr int kVnWaves = 16;                 // wavefronts per VN workgroup
-constexpr int kPv = 4;                       // VN column-sum loads in flight
+#ifndef LDPC_PV
+#define LDPC_PV 4
+#endif
+constexpr int kPv = LDPC_PV;                 // VN column-sum loads in flight
 
 __device__ __forceinline__ int uniform(int x) { return __builtin_amdgcn_readfirstlane(x); }
 
