@@ -163,6 +163,7 @@ void state_bind(ldpc_decoder *d, int ntiles, int count) {
     s.E = d->E;
     s.T = d->T;
     s.rare_count = d->rare;
+    s.active_count = nullptr;
     s.rare_list = d->rare + 2;
     s.nslots = d->nslots;
     s.L = d->L;
@@ -205,14 +206,36 @@ hipError_t timed(ldpc_decoder *d, int kind, hipStream_t s, F &&fn) {
     return e;
 }
 
-hipError_t run_iterations(ldpc_decoder *d, const DevGraph &G, const DevState &st, int max_iter, bool nllr,
-                          hipStream_t s) {
+// Up to max_iter CN/VN sweeps.  With poll (callers that synchronise anyway),
+// the host reads how many tiles are still running after VN(it) for it < 4 and
+// every 4th iteration after, and stops once none is: launches over finished
+// tiles cost ~0.3 ms each (a grid of early-exiting workgroups).
+hipError_t run_iterations(ldpc_decoder *d, const DevGraph &G, const DevState &st_in, int max_iter, bool nllr,
+                          hipStream_t s, bool poll) {
     hipError_t e = hipSuccess;
+    DevState st = st_in;
+    if (poll) {
+        if (d->pactive_cap < max_iter) {
+            (void)hipFree(d->pactive);
+            d->pactive = nullptr;
+            d->pactive_cap = 0;
+            if (hipMalloc((void **)&d->pactive, sizeof(int) * max_iter) != hipSuccess) return hipErrorOutOfMemory;
+            d->pactive_cap = max_iter;
+        }
+        if ((e = hipMemsetAsync(d->pactive, 0, sizeof(int) * max_iter, s))) return e;
+        st.active_count = d->pactive;
+    }
     for (int it = 0; it < max_iter && e == hipSuccess; ++it) {
         e = timed(d, LDPC_K_CN, s, [&] { return ldpc::launch_cn(G, st, it, s); });
         if (e == hipSuccess) e = ldpc::launch_cn_rare(G, st, it, s);
         if (e == hipSuccess)
             e = timed(d, LDPC_K_VN, s, [&] { return ldpc::launch_vn(G, st, it, max_iter, nllr, s); });
+        if (e == hipSuccess && poll && it + 1 < max_iter && (it < 4 || (it + 1) % 4 == 0)) {
+            int running = 0;
+            e = hipMemcpyAsync(&running, d->pactive + it, sizeof(int), hipMemcpyDeviceToHost, s);
+            if (e == hipSuccess) e = hipStreamSynchronize(s);
+            if (e == hipSuccess && running == 0) break;
+        }
     }
     return e;
 }
@@ -530,7 +553,7 @@ int ldpc_decode_f64(ldpc_decoder *d, int32_t batch, const double *llr, int32_t m
         }
         if ((e = ldpc::launch_reset(G, st, s))) return fail_dev(e, "reset");
         if ((e = ldpc::launch_load_llr(G, st, src, s))) return fail_dev(e, "load");
-        if ((e = run_iterations(d, G, st, max_iter, nllr, s))) return fail_dev(e, "iteration");
+        if ((e = run_iterations(d, G, st, max_iter, nllr, s, !dev_ptrs))) return fail_dev(e, "iteration");
         uint8_t *zdst = dev_ptrs ? (z_out ? z_out + (size_t)start * n : nullptr) : d->z_stage;
         double *pdst = dev_ptrs ? (post_out ? post_out + (size_t)start * n : nullptr) : (post_out ? d->post_stage : nullptr);
         if (zdst || pdst) {
@@ -669,7 +692,9 @@ int mc_stream_point(ldpc_decoder *d, uint64_t seed, int p, double sigma, int64_t
     constexpr int kPoll = 4;
     int64_t step = 0;
     for (;;) {
-        const int64_t until = std::max<int64_t>(step + kPoll, min_steps);
+        // every frame fits in the slots: all start now and stop by max_iter
+        const int64_t until = total <= slots ? std::max<int64_t>(step + kPoll, max_iter)
+                                             : std::max<int64_t>(step + kPoll, min_steps);
         for (; step < until; ++step) {
             const int par = (int)(step & 1);
             HIP_TRY(timed(d, LDPC_K_CN, s, [&] { return ldpc::launch_cn(G, st, par, s, true); }));
@@ -725,7 +750,7 @@ int ldpc_mc_run(ldpc_decoder *d, uint64_t seed, int32_t n_points, const double *
             HIP_TRY(timed(d, LDPC_K_GEN, s,
                           [&] { return ldpc::launch_frames(G, st, phys_tile(d), seed, p, sigmas[p], frame0 + start,
                                                            ldpc::kFramesCh, nullptr, s); }));
-            HIP_TRY(run_iterations(d, G, st, max_iter, nllr, s));
+            HIP_TRY(run_iterations(d, G, st, max_iter, nllr, s, true));
             HIP_TRY(timed(d, LDPC_K_COUNT, s, [&] {
                 return ldpc::launch_count(G, st, d->counters + (size_t)p * LDPC_MC_NCOUNT, s);
             }));

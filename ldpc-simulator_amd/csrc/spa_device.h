@@ -41,6 +41,7 @@ struct DevState {
     int *fresh, *refill;     // streaming Monte-Carlo: lane holds a new frame / lane wants one
     int *rare_list;          // [ntiles*m] tile*m+row of rows left to cn_rare_kernel
     int *rare_count;         // [2] per iteration parity
+    int *active_count;       // [max_iter] or null: vn_kernel adds the tiles still running after it
     int nslots;
     uint32_t *ubits;         // MC only (may be null)
     double *nllr_hist;       // [frame][hist_stride] or null

@@ -529,7 +529,10 @@ __global__ __launch_bounds__(1024) void vn_kernel(DevGraph g, DevState st, int i
         }
     }
     const unsigned long long any = __ballot(still);
-    if (lane == 0) st.tile_active[tile] = any != 0ull ? 1 : 0;
+    if (lane == 0) {
+        st.tile_active[tile] = any != 0ull ? 1 : 0;
+        if (any && st.active_count) atomicAdd(&st.active_count[it], 1);  // host poll: 0 -> all stopped
+    }
 }
 
 // ------------------------------------------------------------ plumbing kernels
