@@ -42,9 +42,12 @@ def parse():
     ap.add_argument("--code", default="wimax_576_0.5")
     ap.add_argument("--frames", type=int, default=65536, help="frames per GPU per step")
     ap.add_argument("--chunk", type=int, default=0, help="decoder slots (frames resident at once); 0 = whole batch")
-    ap.add_argument("--schedule", choices=("stream", "static"), default="stream",
+    ap.add_argument("--schedule", choices=("auto", "stream", "static"), default="auto",
                     help="stream: a slot takes the next frame as soon as its frame stops; static: chunks decoded "
-                         "to completion (same frames, same counters)")
+                         "to completion (same frames, same counters); auto: static where the tile-resident "
+                         "decoder applies (one launch per chunk, tiles exit on their own), else stream")
+    ap.add_argument("--split", action="store_true",
+                    help="parity mode: per-iteration CN/VN launches even where the tile-resident decoder applies")
     ap.add_argument("--iters", type=int, default=50)
     ap.add_argument("--snr", type=float, default=0.0, help="reference SNR axis (dB), speed=1")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU-baseline sample budget (0 = skip)")
@@ -106,7 +109,7 @@ def max_over_ranks(dist, x, local):
     return float(t.item())
 
 
-def committed_traffic(nnz, frames):
+def committed_traffic(nnz, frames, kernel="cn"):
     """HBM bytes per cn_kernel launch from the newest committed PMC pass
     (profiles/*/traffic.json, tools/profile.sh + tools/summarize_profile.py)
     for this exact workload shape, or (None, None)."""
@@ -119,8 +122,9 @@ def committed_traffic(nnz, frames):
         t = json.load(open(f))
         if t.get("edges") == nnz and t.get("frames") == frames:
             k = t["kernels"]
-            cn = k.get("cn") or k.get("cn_kernel<false>")
-            best = (cn["traffic_bytes"], os.path.relpath(f, ROOT))
+            cn = k.get(kernel) or (k.get("cn_kernel<false>") if kernel == "cn" else None)
+            if cn:
+                best = (cn["traffic_bytes"], os.path.relpath(f, ROOT))
     return best or (None, None)
 
 
@@ -210,6 +214,10 @@ def main():
         pgraph = Graph(Hphys, device=local) if Hphys is not None else None
     chunk = args.chunk or args.frames
     dec = Decoder(graph, chunk)
+    if args.schedule == "auto":
+        from ldpc_amd import _lib
+        tile_ok = pgraph is None and not args.split and _lib.lib().ldpc_tile_lds_bytes(graph.handle) > 0
+        args.schedule = "static" if tile_ok else "stream"
     sigma = 1.0 / math.sqrt(2.0 * 1.0 * (10.0 ** (args.snr * 0.1)))  # channel.py:113
     B = args.frames
 
@@ -220,7 +228,7 @@ def main():
         if pgraph is not None:
             c = dec.phys_mc_run(pgraph, SEED, [sigma], B, frame0, args.iters, hbm=args.phys_hbm)
         else:
-            c = dec.mc_run(SEED, [sigma], B, frame0, args.iters, static=args.schedule == "static")
+            c = dec.mc_run(SEED, [sigma], B, frame0, args.iters, static=args.schedule == "static", split=args.split)
         if record:
             local_totals[:] += c
         return allreduce_counters(dist, c, local)
@@ -264,6 +272,11 @@ def main():
     decode_gbs = dec_bytes / (decode_ms / 1e3) / 1e9 if decode_ms else 0.0
     traffic, traffic_src = committed_traffic(nnz, chunk)
 
+    tile_ms, tile_launches = prof.get("tile", (0.0, 0))
+    if tile_launches:  # tile-resident decoder: one launch decodes a chunk through all its iterations
+        cn_name = "tile_kernel"
+        decode_ms = tile_ms
+        decode_gbs = dec_bytes / (decode_ms / 1e3) / 1e9 if decode_ms else 0.0
     out = {
         "metric": METRIC,
         "value": cw_s,
@@ -297,10 +310,22 @@ def main():
             "bytes_model": "16 B x H_std edges x frame-iterations executed (E_old read + E_new write)",
         },
         "decode_roofline": {"achieved_GBs": decode_gbs, "frac": decode_gbs / HBM_PEAK_GBS,
-                            "cn_ms": cn_ms, "vn_ms": vn_ms, "gen_ms": prof["generate"][0],
+                            "cn_ms": cn_ms, "vn_ms": vn_ms, "tile_ms": tile_ms, "gen_ms": prof["generate"][0],
                             "count_ms": prof["count"][0]},
         "cpu_baseline": None,
     }
+    if tile_launches and pgraph is None:
+        # the whole decode is one kernel: algorithmic bytes per decoded frame
+        # 8n + sum_iters 16 E + ceil(n/8) + 8, over this rank's frames, per launch
+        out["roofline"] = {
+            "bound": "hbm", "achieved": decode_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": decode_gbs / HBM_PEAK_GBS, "traffic": committed_traffic(nnz, chunk, "tile")[0],
+            "traffic_source": committed_traffic(nnz, chunk, "tile")[1],
+            "kernel": "tile_kernel", "launches": tile_launches, "avg_launch_ms": tile_ms / tile_launches,
+            "bytes_per_launch": dec_bytes / tile_launches,
+            "bytes_model": "per frame 8 n (channel LLRs) + 16 B x H_std edges x iterations executed "
+                           "(E_old read + E_new write) + ceil(n/8) + 8 (SURVEY 8d); CN and VN fused",
+        }
     if pgraph is not None:  # physical mode (not the reference's arithmetic: §8 f4)
         pnnz = int(pgraph.nnz)
         pms, pl = prof["phys"]

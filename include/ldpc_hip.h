@@ -45,6 +45,8 @@ extern "C" {
 #define LDPC_F_DEVICE_PTRS 0x2u /* I/O pointers are device pointers, async        */
 #define LDPC_F_STATIC 0x4u      /* ldpc_mc_run: chunked schedule, no slot refill  */
 #define LDPC_F_PHYS_HBM 0x8u    /* physical mode: HBM-resident state even if LDS fits */
+#define LDPC_F_SPLIT 0x10u      /* parity decoder: separate CN/VN launches per iteration even
+                                   where the tile-resident decoder applies (A/B, tests) */
 
 typedef struct ldpc_hstd ldpc_hstd;       /* standard-form parity-check matrix  */
 typedef struct ldpc_graph ldpc_graph;     /* H_std uploaded to one GPU          */
@@ -87,6 +89,13 @@ int ldpc_graph_destroy(ldpc_graph *g);
  * ("cn_row_kernel": rows of degree <= 192 kept in registers, 16 B/edge;
  * "cn_kernel": one wavefront per row, 24 B/edge) -- measurement labels. */
 const char *ldpc_cn_kernel_name(const ldpc_graph *g);
+/* LDS bytes per workgroup of the tile-resident decoder for this graph, or 0 if
+ * it does not apply (it needs H_std = [A | I_m], row degree <= 192 and the A
+ * column sums of 64 frames in LDS: k*512 B + ~13 KB <= 160 KB, e.g.
+ * wimax_576_0.5).  Where it applies, ldpc_decode_f64 and the static schedule of
+ * ldpc_mc_run decode a whole chunk in ONE launch (tile_kernels.hip); the
+ * separate per-iteration launches remain available via LDPC_F_SPLIT. */
+int64_t ldpc_tile_lds_bytes(const ldpc_graph *g);
 /* Physical-mode kernel for this (sparse) graph: "phys_reg_kernel" / "phys_kernel"
  * (state in LDS) or "phys_cn_tile_kernel" (state in HBM). */
 const char *ldpc_phys_kernel_name(const ldpc_graph *g, uint32_t flags);
@@ -198,7 +207,8 @@ int ldpc_phys_mc_run(ldpc_decoder *d_std, const ldpc_graph *g_phys, uint64_t see
 #define LDPC_K_PHYS 4
 #define LDPC_K_PHYS_CN 5
 #define LDPC_K_PHYS_VN 6
-#define LDPC_K_NKINDS 7
+#define LDPC_K_TILE 7 /* tile-resident decoder: all iterations of a chunk */
+#define LDPC_K_NKINDS 8
 int ldpc_profile_enable(ldpc_decoder *d, int enable);
 int ldpc_profile_read(ldpc_decoder *d, double *ms_out, int64_t *launches_out);
 

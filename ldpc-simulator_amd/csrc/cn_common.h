@@ -1,0 +1,62 @@
+// cn_common.h -- device pieces shared by the parity-mode check-node kernels
+// (spa_kernels.hip: cn_kernel / cn_row_kernel / cn_rare_kernel;
+// tile_kernels.hip: the tile-resident decoder): the reference's clip constants,
+// numpy's tanh with its coefficient table staged in LDS, and the atanh log table.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "spa_math.h"
+
+namespace ldpc {
+namespace {
+
+constexpr double kCL = 0.99999999999999878;  // spa_decoder.py:141,167
+constexpr double kTiny = 1e-10;              // spa_decoder.py:159
+__device__ __forceinline__ int uniform(int x) { return __builtin_amdgcn_readfirstlane(x); }
+
+// np.clip(q, -CL, CL) as v_max_f64 + v_min_f64 (2 VALU instead of 2 compares
+// and 4 selects).  Differs from np.clip only for NaN, which a message cannot
+// be for finite or infinite channel LLRs (|t| <= 1, |E| <= 35.04).
+__device__ __forceinline__ double clip_cl(double q) { return fmin(fmax(q, -kCL), kCL); }
+
+// ---- math tables in LDS (9 x 16 tanh pairs + 128 log entries = 6.4 KB)
+struct LdsTanh {
+    const Pair *p;
+    __device__ __forceinline__ Pair operator()(int pp, int i) const { return p[pp * 16 + i]; }
+};
+struct alignas(16) LogEntry4 {
+    double invc, hi, lo, pad;
+};
+struct LdsLog {
+    const LogEntry4 *e;
+    __device__ __forceinline__ LogEntry operator()(int i) const {
+        const LogEntry4 v = e[i];
+        return {v.invc, v.hi, v.lo};
+    }
+};
+struct MathLds {
+    Pair tanh[9 * 16];
+    LogEntry4 log[128];
+};
+
+__device__ __forceinline__ void fill_math_lds(MathLds &m) {
+    for (int k = threadIdx.x; k < 9 * 16; k += blockDim.x) {
+        const int pp = k >> 4, i = k & 15;
+        m.tanh[k] = pp == 0 ? Pair{dfrom(tab::kTanhB[i]), dfrom(tab::kTanhC[0][i])}
+                            : Pair{dfrom(tab::kTanhC[2 * pp - 1][i]), dfrom(tab::kTanhC[2 * pp][i])};
+    }
+    for (int i = threadIdx.x; i < 128; i += blockDim.x)
+        m.log[i] = {dfrom(tab::kLog[i][0]), dfrom(tab::kLog[i][1]), dfrom(tab::kLog[i][2]), 0.0};
+}
+
+__device__ __forceinline__ double cn_tanh(double M, const LdsTanh &t) {
+    const double d = M * 0.5;  // == M/2.0 bit for bit (power-of-two scale)
+#ifdef LDPC_DIAG_NOMATH  // diagnostic build only: memory pattern without the math
+    return d * 0.25 + 0.5;
+#endif
+    return d > 17.5 ? kCL : (d < -17.5 ? -kCL : np_tanh(d, t));
+}
+
+
+}  // namespace
+}  // namespace ldpc

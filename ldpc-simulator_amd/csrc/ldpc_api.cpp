@@ -211,9 +211,11 @@ hipError_t timed(ldpc_decoder *d, int kind, hipStream_t s, F &&fn) {
 // every 4th iteration after, and stops once none is: launches over finished
 // tiles cost ~0.3 ms each (a grid of early-exiting workgroups).
 hipError_t run_iterations(ldpc_decoder *d, const DevGraph &G, const DevState &st_in, int max_iter, bool nllr,
-                          hipStream_t s, bool poll) {
+                          hipStream_t s, bool poll, bool split) {
     hipError_t e = hipSuccess;
     DevState st = st_in;
+    if (!split && ldpc::use_tile(G) && st.ntiles <= st.nslots)  // one launch: every tile runs to its own exit
+        return timed(d, LDPC_K_TILE, s, [&] { return ldpc::launch_tile(G, st, max_iter, nllr, s); });
     if (poll) {
         if (d->pactive_cap < max_iter) {
             (void)hipFree(d->pactive);
@@ -248,7 +250,8 @@ size_t workspace_bytes(const DevGraph &g, int cap_tiles) {
     const size_t kw = (size_t)((g.k + 31) / 32);
     size_t b = 0;
     b += cap * (size_t)g.nnz * 8;                                   // E
-    b += (size_t)scratch_slots() * g.max_row_deg * kTile * 8;            // T pool
+    const size_t slots = ldpc::use_tile(g) ? std::max(scratch_slots(), cap_tiles) : scratch_slots();
+    b += slots * g.max_row_deg * kTile * 8;  // T pool
     b += 4 * (2 + (size_t)cap_tiles * g.m);                               // rare list
     b += 2 * cap * (size_t)g.n * 8;    // L, ch
     b += (7 * cap + cap_tiles) * 4;    // per-frame ints + tile flags
@@ -401,6 +404,11 @@ const char *ldpc_cn_kernel_name(const ldpc_graph *g) {
     return ldpc::use_cn_row(g->dg) ? "cn_row_kernel" : "cn_kernel";
 }
 
+int64_t ldpc_tile_lds_bytes(const ldpc_graph *g) {
+    if (!g) return 0;
+    return ldpc::use_tile(g->dg) ? (int64_t)ldpc::tile_lds_bytes(g->dg) : 0;
+}
+
 namespace {
 bool phys_use_lds(const DevGraph &P, uint32_t flags);
 }
@@ -442,6 +450,7 @@ int ldpc_decoder_create(const ldpc_graph *g, int32_t max_frames, ldpc_decoder **
     const size_t kw = (size_t)((G.k + 31) / 32);
     int rc = LDPC_OK;
     d->nslots = scratch_slots();  // E and T are allocated on first parity-mode use
+    if (ldpc::use_tile(G)) d->nslots = std::max(d->nslots, d->cap_tiles);  // one scratch slot per tile workgroup
     if (!rc) rc = dev_alloc(&d->rare, 2 + (size_t)d->cap_tiles * G.m);
     if (!rc && hipMemset(d->rare, 0, sizeof(int) * 2) != hipSuccess)
         rc = ldpc_fail(LDPC_EDEVICE, "ldpc_decoder_create: memset failed");
@@ -553,7 +562,8 @@ int ldpc_decode_f64(ldpc_decoder *d, int32_t batch, const double *llr, int32_t m
         }
         if ((e = ldpc::launch_reset(G, st, s))) return fail_dev(e, "reset");
         if ((e = ldpc::launch_load_llr(G, st, src, s))) return fail_dev(e, "load");
-        if ((e = run_iterations(d, G, st, max_iter, nllr, s, !dev_ptrs))) return fail_dev(e, "iteration");
+        if ((e = run_iterations(d, G, st, max_iter, nllr, s, !dev_ptrs, flags & LDPC_F_SPLIT)))
+            return fail_dev(e, "iteration");
         uint8_t *zdst = dev_ptrs ? (z_out ? z_out + (size_t)start * n : nullptr) : d->z_stage;
         double *pdst = dev_ptrs ? (post_out ? post_out + (size_t)start * n : nullptr) : (post_out ? d->post_stage : nullptr);
         if (zdst || pdst) {
@@ -750,7 +760,7 @@ int ldpc_mc_run(ldpc_decoder *d, uint64_t seed, int32_t n_points, const double *
             HIP_TRY(timed(d, LDPC_K_GEN, s,
                           [&] { return ldpc::launch_frames(G, st, phys_tile(d), seed, p, sigmas[p], frame0 + start,
                                                            ldpc::kFramesCh, nullptr, s); }));
-            HIP_TRY(run_iterations(d, G, st, max_iter, nllr, s, true));
+            HIP_TRY(run_iterations(d, G, st, max_iter, nllr, s, true, flags & LDPC_F_SPLIT));
             HIP_TRY(timed(d, LDPC_K_COUNT, s, [&] {
                 return ldpc::launch_count(G, st, d->counters + (size_t)p * LDPC_MC_NCOUNT, s);
             }));

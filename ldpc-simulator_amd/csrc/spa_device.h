@@ -71,6 +71,12 @@ bool use_cn_row(const DevGraph &g);  // launch_cn runs cn_row_kernel (else cn_ke
 hipError_t launch_cn_rare(const DevGraph &g, const DevState &st, int it, hipStream_t s, bool stream = false);
 hipError_t launch_vn(const DevGraph &g, const DevState &st, int it, int max_iter, bool nllr, hipStream_t s,
                      unsigned long long *stream_ctr = nullptr);
+// tile-resident decoder (tile_kernels.hip): all iterations of a tile in one
+// workgroup, check- and variable-node updates fused; [A | I_m] graphs whose A
+// column sums fit in LDS (tile_lds_bytes > 0).  Needs st.ntiles <= st.nslots.
+size_t tile_lds_bytes(const DevGraph &g);
+bool use_tile(const DevGraph &g);
+hipError_t launch_tile(const DevGraph &g, const DevState &st, int max_iter, bool nllr, hipStream_t s);
 hipError_t launch_stream_init(const DevGraph &g, const DevState &st, hipStream_t s);
 hipError_t launch_refill(const DevGraph &g, const DevState &st, uint64_t seed, int snr_point, double sigma,
                          int64_t frame0, int64_t total, unsigned long long *next, hipStream_t s);

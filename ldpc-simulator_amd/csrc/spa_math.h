@@ -119,19 +119,31 @@ __host__ __device__ __forceinline__ double fast_rcp(double d) {
 #endif
 }
 
+// atanh(a) for 0 <= a < 2^-5: odd Taylor polynomial (the small branch of atanh_f)
+__host__ __device__ __forceinline__ double atanh_small_abs(double a, const AtanhCoef &c = kAtanhCoef) {
+    const double a2 = a * a;
+    double p = __builtin_fma(a2, c.t13, c.t11);
+    p = __builtin_fma(p, a2, c.t9);
+    p = __builtin_fma(p, a2, c.t7);
+    p = __builtin_fma(p, a2, c.t5);
+    p = __builtin_fma(p, a2, c.t3);
+    return __builtin_fma(a * a2, p, a);
+}
+constexpr double kAtanhSmall = 0x1p-5;  // atanh_f's Taylor / log switch
+
+// atanh(q) for |q| < 2^-5 only; equals atanh_f(q) bit for bit there
+__host__ __device__ __forceinline__ double atanh_small(double q, const AtanhCoef &c = kAtanhCoef) {
+    const double res = atanh_small_abs(__builtin_fabs(q), c);
+    return dfrom(dbits(res) | (dbits(q) & 0x8000000000000000ull));
+}
+
 // atanh(q) for |q| <= CL.
 template <class LogTab>
 __host__ __device__ __forceinline__ double atanh_f(double q, const LogTab &lt, const AtanhCoef &c = kAtanhCoef) {
     const double a = __builtin_fabs(q);
     double res;
-    if (a < 0x1p-5) {
-        const double a2 = a * a;
-        double p = __builtin_fma(a2, c.t13, c.t11);
-        p = __builtin_fma(p, a2, c.t9);
-        p = __builtin_fma(p, a2, c.t7);
-        p = __builtin_fma(p, a2, c.t5);
-        p = __builtin_fma(p, a2, c.t3);
-        res = __builtin_fma(a * a2, p, a);
+    if (a < kAtanhSmall) {
+        res = atanh_small_abs(a, c);
     } else {
         // atanh(a) = log(y)/2, y = (1+a)/(1-a) carried as y_hi + y_lo:
         // u = 1+a and v = 1-a are rounded, their errors cu, cv exact (u-1, v-1

@@ -1,0 +1,563 @@
+// tile_kernels.hip -- the tile-resident parity decoder (gfx950).
+//
+// One workgroup (16 wavefronts, lane = frame) decodes one tile of 64 frames
+// through ALL its iterations of python_ldpc_app/spa_decoder.py:104-276, with
+// the check-node update (:112-168), the variable-node sum (:173-185), the hard
+// decision / syndrome / early termination (:188-253) and the M update
+// (:260-268) in one launch.  For graphs H_std = [A | I_m] whose column sums of
+// the A part fit in LDS (k x 64 frames x 8 B: wimax_576_0.5, k = 288 ->
+// 144 KB), the variable-node pass needs no second sweep over E:
+//
+//   rows are processed in ascending order, so the sum of column j,
+//   S_j = ((0 + E_r0j) + E_r1j) + ...  rows ascending (scipy csr_matvec of
+//   E^T, the reference's rounding order), is accumulated in LDS as each row's
+//   new messages are produced.  Identity column k+r has one edge (row r):
+//   its posterior ch + (0 + E) is final when row r is.
+//
+// HBM traffic per edge and iteration is the algorithmic 16 B (E_old read +
+// E_new write) plus the posterior gather L[col] (served by L2/MALL: a tile's
+// L is 295 KB); the separate CN/VN launches move 24 B + the gather.
+//
+// Within a row (degree <= 192) wavefront w owns the contiguous chunk of
+// C = ceil(deg/16) edges starting at position w*C and keeps their t in
+// registers.  P = t0*t1*... is formed strictly left to right by handing the
+// running product from wavefront to wavefront through an LDS slot guarded by
+// an epoch-tagged flag (no workgroup barrier).  Each wavefront runs the
+// software pipeline
+//
+//   body(r):  P3(r-1)  E_new = 2 atanh(clip(P/t)) of its chunk of row r-1,
+//                      stores E_new, adds it into S (or writes the identity
+//                      column's posterior);
+//             hop(r)   waits for wavefront w-1's product of row r, multiplies
+//                      its chunk in, publishes;
+//             P1(r+1)  loads L[col] and E_old of its chunk of row r+1,
+//                      t = tanh((L - E_old)/2).
+//
+// Ordering of the S additions: any P3(r) waits for the final product of row r,
+// published by the last hop(r); every wavefront's hop(r) follows its own
+// P3(r-1) in program order, so all additions of row r-1 precede any of row r
+// (a column occurs once per row, so no two additions of one row collide).
+// The same argument lets two chain slots serve all rows.
+//
+// Rare rows (some |t| <= 1e-10, spa_decoder.py:159-164): every wavefront parks
+// its t in the workgroup's scratch slot (global, read back through L2) and
+// the "product of the others" is walked there.
+//
+// End of a pass: L_j = ch_j + S_j for the A columns (the normalized-LLR count
+// :210-228 against the previous posterior), the z^1 bit vectors of all
+// columns in LDS, one sweep over the rows for the syndrome, and the per-frame
+// exit decisions of vn_kernel (static schedule).  The tile stops when none of
+// its frames is running.
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstdlib>
+
+#include "cn_common.h"
+#include "spa_device.h"
+#include "spa_math.h"
+
+namespace ldpc {
+namespace {
+
+constexpr int kTW = 16;  // wavefronts per workgroup
+constexpr int kTK = 12;  // edges per wavefront chunk: row degree <= kTW * kTK = 192
+constexpr int kTR = 2;   // chain slots (see the ordering argument above)
+constexpr size_t kTileLdsMax = 163840;
+
+// Dynamic LDS carve (bytes); every region 16-B aligned.
+struct TileLayout {
+    size_t S, math, slot, zb, ib, lane_i, flags, total;
+};
+__host__ __device__ inline size_t al16(size_t x) { return (x + 15) & ~(size_t)15; }
+__host__ __device__ inline TileLayout tile_layout(int k, int m) {
+    TileLayout t;
+    size_t o = 0;
+    t.S = o;
+    o = al16(o + (size_t)k * kTile * sizeof(double));
+    t.math = o;
+    o = al16(o + sizeof(MathLds));
+    t.slot = o;
+    o = al16(o + (size_t)kTR * kTile * sizeof(double));
+    t.zb = o;
+    o = al16(o + (size_t)((k + 31) / 32) * kTile * sizeof(uint32_t));
+    t.ib = o;
+    o = al16(o + (size_t)((m + 31) / 32) * kTile * sizeof(uint32_t));
+    t.lane_i = o;  // bad[64], nllr count[64], live[64]
+    o = al16(o + 3 * kTile * sizeof(int));
+    t.flags = o;  // chain flag[kTR], tiny[kTR], tiny sequence, tile running
+    o = al16(o + (2 * kTR + 2) * sizeof(int));
+    t.total = o;
+    return t;
+}
+
+__device__ __forceinline__ int lds_ld(const int *p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void lds_st(int *p, int v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+// LDS-only fences: order this wavefront's LDS accesses around a flag without
+// waiting for its outstanding global stores.
+__device__ __forceinline__ void lds_release() { __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local"); }
+__device__ __forceinline__ void lds_acquire() { __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local"); }
+// Compile-time knobs (A/B builds only): LDPC_TILE_SLEEP polls with s_sleep 1
+// between flag reads; LDPC_TILE_PRIO raises the wavefront's issue priority
+// while it carries the product chain; LDPC_TILE_DIAG_NOCHAIN (diagnostic,
+// WRONG results) skips every wait to time the pipeline without the chain.
+#ifndef LDPC_TILE_SLEEP
+#define LDPC_TILE_SLEEP 1
+#endif
+#ifndef LDPC_TILE_PRIO
+#define LDPC_TILE_PRIO 0
+#endif
+__device__ __forceinline__ void wait_flag(const int *p, int v) {
+#ifndef LDPC_TILE_DIAG_NOCHAIN
+    while (uniform(lds_ld(p)) != v) {
+        if (LDPC_TILE_SLEEP) __builtin_amdgcn_s_sleep(1);
+    }
+#endif
+    lds_acquire();
+}
+// Load through L2 (not this CU's L1): data another wavefront of the workgroup
+// stored (posteriors, rare-row scratch).
+__device__ __forceinline__ double ld_l2(const double *p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Compile-time layout/schedule switches (A/B builds; defaults = measured best):
+//   LDPC_TILE_SADDR     1: tile accesses as uniform base + 32-bit byte offset
+//                       (saddr form); 0: per-lane 64-bit pointers
+//   LDPC_TILE_P3FUSED   1: each edge's E_new computed and stored in one loop;
+//                       0: all E_new of the chunk first, then the stores
+//   LDPC_TILE_PREFETCH  1: the next P1's loads are issued inside this P3;
+//                       0: P1 issues its loads after the hop, in STAGES groups
+#ifndef LDPC_TILE_SADDR
+#define LDPC_TILE_SADDR 0
+#endif
+#ifndef LDPC_TILE_P3FUSED
+#define LDPC_TILE_P3FUSED 0
+#endif
+#ifndef LDPC_TILE_PREFETCH
+#define LDPC_TILE_PREFETCH 0
+#endif
+#ifndef LDPC_TILE_STAGES
+#define LDPC_TILE_STAGES 1
+#endif
+//   LDPC_TILE_TANH_BF   1: tanh evaluated for every lane, the +-17.5 clip as
+//                       selects (straight-line code across the chunk's edges)
+//   LDPC_TILE_SMALLQ    1: all q = clip(P/t) of the chunk first; if no lane of
+//                       the wavefront has |q| >= 2^-5 (every edge at 0 dB),
+//                       the whole chunk takes atanh's Taylor branch as one
+//                       straight-line block, else atanh_f per edge
+#ifndef LDPC_TILE_TANH_BF
+#define LDPC_TILE_TANH_BF 1
+#endif
+#ifndef LDPC_TILE_SMALLQ
+#define LDPC_TILE_SMALLQ 0
+#endif
+
+// element (item, lane) of a tile array
+template <class T>
+__device__ __forceinline__ T *at(T *base, int item, uint32_t lane) {
+    if (LDPC_TILE_SADDR) {
+        const uint32_t off = ((uint32_t)item * kTile + lane) * (uint32_t)sizeof(T);
+        return (T *)((char *)base + off);
+    }
+    return base + (size_t)item * kTile + lane;
+}
+
+struct RowChunk {
+    int beg, deg, C, c0, cnt;
+};
+__device__ __forceinline__ RowChunk chunk_of(const int *__restrict__ row_ptr, int r, int wave) {
+    RowChunk c;
+    c.beg = row_ptr[r];
+    c.deg = row_ptr[r + 1] - c.beg;
+    c.C = (c.deg + kTW - 1) / kTW;
+    c.c0 = c.beg + wave * c.C;
+    c.cnt = max(0, min(c.deg - wave * c.C, c.C));
+    return c;
+}
+
+struct TileCtx {
+    const int *__restrict__ col_idx;
+    const int *__restrict__ row_ptr;
+    // tile bases (uniform); element (item, lane) at [item * 64 + lane]
+    double *Eb;        // messages E
+    double *Lb;        // posteriors
+    const double *Cb;  // channel LLRs
+    double *Tb;        // rare-row scratch slot of this workgroup
+    double *S;         // LDS [k][64]
+    double *slot;      // LDS [kTR][64]
+    uint32_t *ib;      // LDS [mw][64] z^1 of the identity columns
+    int *flag, *tinyf, *tseq;
+    LdsTanh ttab;
+    LdsLog ltab;
+    AtanhCoef ac;
+    int k, wave;
+    uint32_t lane;
+    int ep0;  // epoch of row 0 in this pass (flags are tagged (epoch, stage))
+    bool first, live;
+    int ntiny;
+};
+
+// P1 pieces: L[col] of edge i of chunk rc, E_old, and t = tanh((L - E_old)/2).
+// Loads are unconditional (index clamped into the chunk).
+__device__ __forceinline__ double tile_load_l(const TileCtx &c, const RowChunk &rc, int i) {
+    const double *Ls = c.first ? c.Cb : c.Lb;
+    return ld_l2(at(Ls, c.col_idx[rc.c0 + min(i, rc.cnt - 1)], c.lane));
+}
+__device__ __forceinline__ double tile_load_e(const TileCtx &c, const RowChunk &rc, int i) {
+    return c.first ? 0.0 : *at(c.Eb, rc.c0 + min(i, rc.cnt - 1), c.lane);
+}
+__device__ __forceinline__ bool tile_t(const TileCtx &c, double &t, double eo) {
+    const double M = c.first ? t : t - eo;  // :85-90 / :260-268
+    if (LDPC_TILE_TANH_BF) {
+        const double d = M * 0.5;
+        const double r = np_tanh(d, c.ttab);
+        t = d > 17.5 ? kCL : (d < -17.5 ? -kCL : r);  // :138-146 (cn_tanh, as selects)
+    } else {
+        t = cn_tanh(M, c.ttab);
+    }
+    return !(fabs(t) > kTiny);
+}
+
+// P1 with its own loads, in STAGES groups; returns whether some lane has
+// |t| <= 1e-10.
+__device__ __forceinline__ bool tile_p1(const TileCtx &c, const RowChunk &rc, double (&t)[kTK]) {
+    bool tiny = false;
+    if (rc.cnt > 0) {
+        constexpr int H = (kTK + LDPC_TILE_STAGES - 1) / LDPC_TILE_STAGES;
+#pragma unroll
+        for (int h = 0; h < LDPC_TILE_STAGES; ++h) {
+            double eo[H];
+#pragma unroll
+            for (int i = h * H; i < min((h + 1) * H, kTK); ++i) {
+                t[i] = tile_load_l(c, rc, i);
+                eo[i - h * H] = tile_load_e(c, rc, i);
+            }
+#pragma unroll
+            for (int i = h * H; i < min((h + 1) * H, kTK); ++i)
+                if (i < rc.cnt) tiny |= tile_t(c, t[i], eo[i - h * H]);
+        }
+    }
+    return __ballot(tiny) != 0ull;
+}
+// P1 math on prefetched loads (LDPC_TILE_PREFETCH)
+__device__ __forceinline__ bool tile_p1_math(const TileCtx &c, const RowChunk &rc, double (&t)[kTK],
+                                             const double (&eo)[kTK]) {
+    bool tiny = false;
+#pragma unroll
+    for (int i = 0; i < kTK; ++i)
+        if (i < rc.cnt) tiny |= tile_t(c, t[i], eo[i]);
+    return __ballot(tiny) != 0ull;
+}
+
+// hop: this wavefront's segment of row r's left-to-right product.
+__device__ __forceinline__ void tile_hop(const TileCtx &c, int r, const double (&t)[kTK], bool tiny) {
+    const RowChunk rc = chunk_of(c.row_ptr, r, c.wave);
+    if (rc.deg == 0) return;  // spa_decoder.py:115-122
+    const int s = r & (kTR - 1);
+    const int ep = ((c.ep0 + r) & 0x3ffffff) * 32;
+    double *sl = c.slot + s * kTile + c.lane;
+    double P;
+    if (LDPC_TILE_PRIO) __builtin_amdgcn_s_setprio(2);
+    if (c.wave == 0) {
+        P = t[0];  // wavefront 0 always holds the row's first edge
+#pragma unroll
+        for (int i = 1; i < kTK; ++i)
+            if (i < rc.cnt) P = P * t[i];
+        if (c.lane == 0) lds_st(c.tinyf + s, tiny ? 1 : 0);
+    } else {
+        wait_flag(c.flag + s, ep + c.wave);
+        P = *sl;
+#pragma unroll
+        for (int i = 0; i < kTK; ++i)
+            if (i < rc.cnt) P = P * t[i];
+        if (tiny && c.lane == 0) lds_st(c.tinyf + s, 1);
+    }
+    *sl = P;
+    lds_release();
+    if (c.lane == 0) lds_st(c.flag + s, ep + c.wave + 1);
+    if (LDPC_TILE_PRIO) __builtin_amdgcn_s_setprio(0);
+}
+
+// P3: E_new of this wavefront's chunk of row r, stored and folded into the
+// column sums (t is overwritten with E_new).  With LDPC_TILE_PREFETCH, as
+// slot i of t is consumed the L[col] load of edge i of the next P1 chunk rc1
+// is issued into it (E_old of rc1 into eo first).
+__device__ __forceinline__ void tile_p3(TileCtx &c, int r, double (&t)[kTK], const RowChunk &rc1,
+                                        double (&eo)[kTK]) {
+    const RowChunk rc = chunk_of(c.row_ptr, r, c.wave);
+    const bool pf = LDPC_TILE_PREFETCH && rc1.cnt > 0;
+    if (pf) {
+#pragma unroll
+        for (int i = 0; i < kTK; ++i) eo[i] = tile_load_e(c, rc1, i);
+    }
+    if (rc.deg == 0) {
+        if (pf) {
+#pragma unroll
+            for (int i = 0; i < kTK; ++i) t[i] = tile_load_l(c, rc1, i);
+        }
+        return;
+    }
+    const int s = r & (kTR - 1);
+    const int ep = ((c.ep0 + r) & 0x3ffffff) * 32;
+    wait_flag(c.flag + s, ep + kTW);
+    const double P = c.slot[s * kTile + c.lane];
+    const bool tiny_row = uniform(lds_ld(c.tinyf + s)) != 0;
+    const bool fused = LDPC_TILE_P3FUSED && !tiny_row;
+    if (!tiny_row && !LDPC_TILE_P3FUSED && LDPC_TILE_SMALLQ) {
+        bool big = false;
+#pragma unroll
+        for (int i = 0; i < kTK; ++i) {
+            if (i < rc.cnt) {
+                t[i] = clip_cl(P / t[i]);  // q (:159-167)
+                big |= !(fabs(t[i]) < kAtanhSmall);
+            }
+        }
+        if (__ballot(big) == 0ull) {
+#pragma unroll
+            for (int i = 0; i < kTK; ++i)
+                if (i < rc.cnt) t[i] = 2.0 * atanh_small(t[i], c.ac);  // :168
+        } else {
+#pragma unroll
+            for (int i = 0; i < kTK; ++i)
+                if (i < rc.cnt) t[i] = 2.0 * atanh_f(t[i], c.ltab, c.ac);
+        }
+    } else if (!tiny_row && !LDPC_TILE_P3FUSED) {
+#pragma unroll
+        for (int i = 0; i < kTK; ++i)
+            if (i < rc.cnt) t[i] = 2.0 * atanh_f(clip_cl(P / t[i]), c.ltab, c.ac);  // :159-168
+    } else if (tiny_row) {
+        // rare: q = prod of the others, in order (np.prod(np.delete(...)), :164)
+        const int pos0 = c.wave * rc.C;
+#pragma unroll
+        for (int i = 0; i < kTK; ++i)
+            if (i < rc.cnt) *at(c.Tb, pos0 + i, c.lane) = t[i];
+        __builtin_amdgcn_s_waitcnt(0);  // scratch stores have reached L2
+        c.ntiny += 1;
+        if (c.lane == 0) __hip_atomic_fetch_add(c.tseq, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        wait_flag(c.tseq, c.ntiny * kTW);
+#pragma unroll
+        for (int i = 0; i < kTK; ++i) {
+            if (i < rc.cnt) {
+                const double ti = t[i];
+                double q;
+                if (fabs(ti) > kTiny) {
+                    q = P / ti;
+                } else {
+                    q = 1.0;
+                    bool fst = true;
+                    for (int p = 0; p < rc.deg; ++p) {
+                        if (p == pos0 + i) continue;
+                        const double t2 = ld_l2(at(c.Tb, p, c.lane));
+                        q = fst ? t2 : q * t2;
+                        fst = false;
+                    }
+                }
+                t[i] = 2.0 * atanh_f(clip_cl(q), c.ltab, c.ac);
+            }
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < kTK; ++i) {
+        if (i < rc.cnt) {
+            if (fused) t[i] = 2.0 * atanh_f(clip_cl(P / t[i]), c.ltab, c.ac);  // :159-168
+            const int e = rc.c0 + i;
+            const int col = c.col_idx[e];
+            if (c.live) *at(c.Eb, e, c.lane) = t[i];
+            if (col < c.k) {  // S_col += E (rows ascending)
+                double *sp = c.S + col * kTile + c.lane;
+                *sp = *sp + t[i];
+            } else {  // identity column: L = ch + (0 + E)  (:173-185)
+                const double Lj = *at(c.Cb, col, c.lane) + (0.0 + t[i]);
+                if (c.live) *at(c.Lb, col, c.lane) = Lj;
+                if (!(Lj < 0.0)) {
+                    const int q = col - c.k;
+                    atomicOr(c.ib + (q >> 5) * kTile + c.lane, 1u << (q & 31));
+                }
+            }
+        }
+        if (pf) t[i] = tile_load_l(c, rc1, i);
+    }
+}
+
+__device__ __forceinline__ void tile_body(TileCtx &c, int r, int m, double (&tcur)[kTK], bool &ycur,
+                                          double (&toth)[kTK], bool &yoth, double (&eo)[kTK]) {
+    RowChunk rc1{};
+    if (r + 1 < m) rc1 = chunk_of(c.row_ptr, r + 1, c.wave);
+    if (r >= 1) tile_p3(c, r - 1, toth, rc1, eo);
+    if (r < m) tile_hop(c, r, tcur, ycur);
+    if (r + 1 < m) {
+        if (LDPC_TILE_PREFETCH && r >= 1) {
+            yoth = tile_p1_math(c, rc1, toth, eo);
+        } else {
+            yoth = tile_p1(c, rc1, toth);
+        }
+    }
+}
+
+__global__ __launch_bounds__(64 * kTW, 1) void tile_kernel(DevGraph g, DevState st, int max_iter, int nllr,
+                                                           const int *__restrict__ col_idx,
+                                                           const int *__restrict__ row_ptr, AtanhCoef ac) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+    const TileLayout ly = tile_layout(g.k, g.m);
+    double *S = (double *)(lds + ly.S);
+    MathLds &mlds = *(MathLds *)(lds + ly.math);
+    uint32_t *zb = (uint32_t *)(lds + ly.zb);
+    uint32_t *ib = (uint32_t *)(lds + ly.ib);
+    int *bad = (int *)(lds + ly.lane_i);
+    int *cntl = bad + kTile;
+    int *livel = cntl + kTile;
+    int *flags = (int *)(lds + ly.flags);
+    const int kw = (g.k + 31) >> 5, mw = (g.m + 31) >> 5;
+    const int tile = blockIdx.x;
+    if (tile >= st.ntiles) return;  // block-uniform
+
+    fill_math_lds(mlds);
+    for (int i = threadIdx.x; i < g.k * kTile; i += blockDim.x) S[i] = 0.0;
+    for (int i = threadIdx.x; i < (kw + mw) * kTile; i += blockDim.x) zb[i] = 0u;  // zb and ib are adjacent
+    for (int i = threadIdx.x; i < 2 * kTile; i += blockDim.x) bad[i] = 0;
+    if (threadIdx.x < 2 * kTR) flags[threadIdx.x] = -1;
+    if (threadIdx.x == 2 * kTR) flags[2 * kTR] = 0;
+    const int lane = threadIdx.x & 63;
+    const int wave = uniform(threadIdx.x >> 6);
+    const int f = tile * kTile + lane;
+    if (wave == 0) livel[lane] = st.done[f] == 0 ? 1 : 0;
+    __syncthreads();
+    if (!st.tile_active[tile]) return;
+
+    TileCtx c;
+    c.col_idx = col_idx;
+    c.row_ptr = row_ptr;
+    c.Eb = st.E + (size_t)tile * g.nnz * kTile;
+    c.Lb = st.L + (size_t)tile * g.n * kTile;
+    c.Cb = st.ch + (size_t)tile * g.n * kTile;
+    c.Tb = st.T + (size_t)blockIdx.x * g.max_row_deg * kTile;
+    c.S = S;
+    c.slot = (double *)(lds + ly.slot);
+    c.ib = ib;
+    c.flag = flags;
+    c.tinyf = flags + kTR;
+    c.tseq = flags + 2 * kTR;
+    c.ttab = LdsTanh{mlds.tanh};
+    c.ltab = LdsLog{mlds.log};
+    c.ac = ac;
+    c.k = g.k;
+    c.lane = lane;
+    c.wave = wave;
+    c.ntiny = 0;
+    const int m = g.m;
+
+    for (int it = 0; it < max_iter; ++it) {
+        c.first = it == 0;
+        c.live = livel[lane] != 0;
+        c.ep0 = it * m;
+        double tA[kTK], tB[kTK], eo[kTK];
+        bool yA = false, yB = false;
+        if (m > 0) yA = tile_p1(c, chunk_of(row_ptr, 0, wave), tA);
+        for (int r = 0; r <= m; r += 2) {
+            tile_body(c, r, m, tA, yA, tB, yB, eo);
+            if (r + 1 <= m) tile_body(c, r + 1, m, tB, yB, tA, yA, eo);
+        }
+        __syncthreads();  // every P3 done: S complete, identity bits set
+
+        // posteriors of the A columns, normalized-LLR count, z^1 bits
+        int my_cnt = 0;
+        for (int j = wave; j < g.k; j += kTW) {
+            double *sp = S + j * kTile + lane;
+            const double Sj = *sp;
+            *sp = 0.0;
+            const double chj = *at(c.Cb, j, lane);
+            const double Lj = chj + Sj;  // channel added after the sum (:173,185)
+            if (nllr) {
+                const double ap = c.first ? chj : ld_l2(at(c.Lb, j, lane));  // a-priori = previous L (:274)
+                my_cnt += (fabs(Lj) <= 7.0 && ap * Lj < 0.0) ? 1 : 0;
+            }
+            if (c.live) *at(c.Lb, j, lane) = Lj;
+            if (!(Lj < 0.0)) atomicOr(zb + (j >> 5) * kTile + lane, 1u << (j & 31));
+        }
+        if (nllr && my_cnt) atomicAdd(cntl + lane, my_cnt);
+        __syncthreads();
+
+        // syndrome of z (:191-204): parity of z^1 over every row
+        uint32_t acc = 0u;
+        for (int r = wave; r < m; r += kTW) {
+            const int b = row_ptr[r], e1 = row_ptr[r + 1];
+            uint32_t par = 0u;
+            for (int e = b; e < e1; ++e) {  // zb and ib are one array: [kw + mw][64]
+                const int col = col_idx[e];
+                const int q = col < g.k ? col : col - g.k;
+                const int w = (q >> 5) + (col < g.k ? 0 : kw);
+                par ^= zb[w * kTile + lane] >> (q & 31);
+            }
+            acc |= par & 1u;
+        }
+        if (acc) atomicOr((uint32_t *)bad + lane, 1u);
+        __syncthreads();
+
+        if (wave == 0) {  // per-frame exits, as vn_kernel (static schedule)
+            bool still = false;
+            if (c.live) {
+                if (nllr) {
+                    const int cn = cntl[lane];
+                    st.nllr_cnt[f] = cn;
+                    if (st.nllr_hist)
+                        st.nllr_hist[(size_t)f * st.hist_stride + it] = g.k > 0 ? (double)cn / g.k : 0.0;
+                }
+                if (bad[lane] == 0) {  // syndrome zero: Result.OK at this iteration (:231-241)
+                    st.done[f] = 1;
+                    st.conv[f] = it;
+                    st.status[f] = 0;
+                    st.iters[f] = it + 1;
+                } else if (it == max_iter - 1) {  // Result.DATA_TRANSFER_NOT_OK (:244-253)
+                    st.done[f] = 1;
+                    st.conv[f] = -1;
+                    st.status[f] = 1;
+                    st.iters[f] = it + 1;
+                } else {
+                    still = true;
+                }
+            }
+            livel[lane] = still ? 1 : 0;
+            bad[lane] = 0;
+            cntl[lane] = 0;
+            const unsigned long long any = __ballot(still);
+            if (lane == 0) {
+                flags[2 * kTR + 1] = any != 0ull ? 1 : 0;
+                if (!any) st.tile_active[tile] = 0;
+            }
+        }
+        for (int i = threadIdx.x; i < (kw + mw) * kTile; i += blockDim.x) zb[i] = 0u;
+        __syncthreads();
+        if (!flags[2 * kTR + 1]) break;
+    }
+}
+
+}  // namespace
+
+size_t tile_lds_bytes(const DevGraph &g) {
+    if (!g.std_form || g.k <= 0 || g.max_row_deg > kTW * kTK) return 0;
+    const size_t b = tile_layout(g.k, g.m).total;
+    return b <= kTileLdsMax ? b : 0;
+}
+
+// LDPC_TILE=0 forces the separate CN/VN launches (A/B, tests)
+bool use_tile(const DevGraph &g) {
+    static const int force = [] {
+        const char *e = getenv("LDPC_TILE");
+        return e ? atoi(e) : -1;
+    }();
+    return force != 0 && tile_lds_bytes(g) > 0;
+}
+
+hipError_t launch_tile(const DevGraph &g, const DevState &st, int max_iter, bool nllr, hipStream_t s) {
+    const size_t lds = tile_lds_bytes(g);
+    if (!lds || st.ntiles > st.nslots) return hipErrorInvalidValue;
+    tile_kernel<<<st.ntiles, 64 * kTW, lds, s>>>(g, st, max_iter, nllr ? 1 : 0, g.col_idx, g.row_ptr, kAtanhCoef);
+    return hipGetLastError();
+}
+
+}  // namespace ldpc

@@ -17,6 +17,7 @@ LDPC_F_NLLR = 0x1
 LDPC_F_DEVICE_PTRS = 0x2
 LDPC_F_STATIC = 0x4
 LDPC_F_PHYS_HBM = 0x8
+LDPC_F_SPLIT = 0x10
 LDPC_MC_NCOUNT = 7
 
 # every symbol include/ldpc_hip.h declares
@@ -24,7 +25,7 @@ EXPORTED = (
     "ldpc_last_error", "ldpc_abi_version", "ldpc_device_count",
     "ldpc_hstd_build", "ldpc_hstd_get", "ldpc_hstd_free",
     "ldpc_graph_create", "ldpc_graph_destroy", "ldpc_graph_info", "ldpc_cn_kernel_name",
-    "ldpc_phys_kernel_name",
+    "ldpc_phys_kernel_name", "ldpc_tile_lds_bytes",
     "ldpc_decoder_bytes", "ldpc_decoder_create", "ldpc_decoder_destroy", "ldpc_decoder_capacity",
     "ldpc_decode_f64", "ldpc_generate_frames", "ldpc_mc_run",
     "ldpc_profile_enable", "ldpc_profile_read",
@@ -62,6 +63,7 @@ def _declare(lib):
         "ldpc_graph_info": (ctypes.c_int, [c_vp, P(c_i32), P(c_i32), P(c_i64), P(c_i32), P(c_i32)]),
         "ldpc_cn_kernel_name": (ctypes.c_char_p, [c_vp]),
         "ldpc_phys_kernel_name": (ctypes.c_char_p, [c_vp, ctypes.c_uint32]),
+        "ldpc_tile_lds_bytes": (ctypes.c_int64, [c_vp]),
         "ldpc_decoder_bytes": (c_i64, [c_vp, c_i32]),
         "ldpc_decoder_create": (ctypes.c_int, [c_vp, c_i32, P(c_vp)]),
         "ldpc_decoder_destroy": (ctypes.c_int, [c_vp]),

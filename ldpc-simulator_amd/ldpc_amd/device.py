@@ -13,7 +13,7 @@ import numpy as np
 from scipy import sparse
 
 from . import _lib
-from ._lib import LDPC_F_NLLR, LDPC_F_PHYS_HBM, LDPC_F_STATIC, LDPC_MC_NCOUNT, as_i32, check
+from ._lib import LDPC_F_NLLR, LDPC_F_PHYS_HBM, LDPC_F_SPLIT, LDPC_F_STATIC, LDPC_MC_NCOUNT, as_i32, check
 
 
 def _csr_arrays(H):
@@ -102,8 +102,11 @@ class Decoder:
     def workspace_bytes(graph, max_frames):
         return int(_lib.lib().ldpc_decoder_bytes(graph.handle, int(max_frames)))
 
-    def decode(self, llr, max_iter, nllr=False, post=False, hist=False, msgs=False):
-        """Decode [B, n] channel LLRs (H_std column order).  Returns numpy arrays."""
+    def decode(self, llr, max_iter, nllr=False, post=False, hist=False, msgs=False, split=False):
+        """Decode [B, n] channel LLRs (H_std column order).  Returns numpy arrays.
+
+        split=True forces the per-iteration CN/VN launches where the
+        tile-resident decoder would run (same results; A/B and tests)."""
         g = self.graph
         llr = np.ascontiguousarray(np.asarray(llr, dtype=np.float64))
         if llr.ndim == 1:
@@ -120,7 +123,7 @@ class Decoder:
         Lp = np.empty((B, g.n), np.float64) if post else None
         hi = np.empty((B, T), np.float64) if (hist and nllr) else None
         E = np.empty((B, g.nnz), np.float64) if msgs else None
-        flags = LDPC_F_NLLR if nllr else 0
+        flags = (LDPC_F_NLLR if nllr else 0) | (LDPC_F_SPLIT if split else 0)
         check("ldpc_decode_f64", _lib.lib().ldpc_decode_f64(
             self._h, B, _lib.ptr(llr), T, flags, _lib.ptr(z), _lib.ptr(conv), _lib.ptr(status),
             _lib.ptr(Lp), _lib.ptr(nl), _lib.ptr(hi), _lib.ptr(iters), _lib.ptr(E), None))
@@ -136,7 +139,7 @@ class Decoder:
             _lib.ptr(u), _lib.ptr(llr), None))
         return u, llr
 
-    def mc_run(self, seed, sigmas, frames_per_point, frame0, max_iter, nllr=False, static=False):
+    def mc_run(self, seed, sigmas, frames_per_point, frame0, max_iter, nllr=False, static=False, split=False):
         """Generate + decode + count on the GPU; returns int64 [n_points, 7] counters.
 
         Default schedule streams frames through the decoder's slots (a slot is
@@ -144,7 +147,7 @@ class Decoder:
         capacity frames to completion.  Same frames, identical counters."""
         sig = np.ascontiguousarray(np.asarray(sigmas, dtype=np.float64))
         out = np.zeros((len(sig), LDPC_MC_NCOUNT), np.int64)
-        flags = (LDPC_F_NLLR if nllr else 0) | (LDPC_F_STATIC if static else 0)
+        flags = (LDPC_F_NLLR if nllr else 0) | (LDPC_F_STATIC if static else 0) | (LDPC_F_SPLIT if split else 0)
         check("ldpc_mc_run", _lib.lib().ldpc_mc_run(
             self._h, int(seed), len(sig), sig.ctypes.data_as(ctypes.POINTER(ctypes.c_double)),
             int(frames_per_point), int(frame0), int(max_iter), flags,
@@ -164,7 +167,7 @@ class Decoder:
             out.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)), None))
         return out
 
-    KINDS = ("cn", "vn", "generate", "count", "phys", "phys_cn", "phys_vn")
+    KINDS = ("cn", "vn", "generate", "count", "phys", "phys_cn", "phys_vn", "tile")
 
     def profile(self, enable=True):
         check("ldpc_profile_enable", _lib.lib().ldpc_profile_enable(self._h, 1 if enable else 0))
