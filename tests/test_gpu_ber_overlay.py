@@ -1,0 +1,27 @@
+"""BER/FER curve overlay against the reference's own Monte-Carlo run
+(north_star: "BER curve overlaying the CPU reference at Eb/N0 1.0-3.0 dB";
+SURVEY.md §8 f1).  The reference curve was measured by running
+python_ldpc_app/main.py (tests/golden/gen_ber_curve.py); its RNG is
+time-seeded, so parity is statistical: the reference's FER and BER at every
+point must lie inside the central 99 % of the GPU's sampling distribution at
+the reference's own frame count B (tests/ber_overlay.py)."""
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def test_ber_curve_overlays_reference(gpu_available):
+    import ber_overlay
+    from conftest import hstd_for
+    from ldpc_amd.device import Decoder, Graph
+
+    dec = Decoder(Graph(hstd_for("wimax_576_0.5"), device=0), 65536)
+    rows = ber_overlay.overlay(dec, groups=200)
+    assert len(rows) == 5 and rows[0]["snr_db"] == 1.0 and rows[-1]["snr_db"] == 3.0
+    for r in rows:
+        print(r)
+        assert r["fer_lo"] <= r["fer_ref"] <= r["fer_hi"], r
+        assert r["ber_lo"] <= r["ber_ref"] <= r["ber_hi"], r
+    # the curve falls: FER strictly decreasing over 1.0 -> 3.0 dB on the GPU
+    fers = [r["fer_gpu"] for r in rows]
+    assert all(a > b for a, b in zip(fers, fers[1:])), fers
