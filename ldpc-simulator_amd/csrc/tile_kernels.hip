@@ -64,6 +64,7 @@ constexpr int kTW = 16;  // wavefronts per workgroup
 constexpr int kTK = 12;  // edges per wavefront chunk: row degree <= kTW * kTK = 192
 constexpr int kTR = 2;   // chain slots (see the ordering argument above)
 constexpr size_t kTileLdsMax = 163840;
+constexpr int kTKW = 10;  // (z^1)_A words per lane held in registers for the syndrome: k <= 320
 
 // Dynamic LDS carve (bytes); every region 16-B aligned.
 struct TileLayout {
@@ -155,6 +156,11 @@ __device__ __forceinline__ double ld_l2(const double *p) {
 #endif
 #ifndef LDPC_TILE_SMALLQ
 #define LDPC_TILE_SMALLQ 0
+#endif
+//   LDPC_TILE_CONST_COEF 1: atanh coefficients as compile-time constants
+//                       instead of kernel-argument SGPRs
+#ifndef LDPC_TILE_CONST_COEF
+#define LDPC_TILE_CONST_COEF 0
 #endif
 
 // element (item, lane) of a tile array
@@ -444,7 +450,7 @@ __global__ __launch_bounds__(64 * kTW, 1) void tile_kernel(DevGraph g, DevState 
     c.tseq = flags + 2 * kTR;
     c.ttab = LdsTanh{mlds.tanh};
     c.ltab = LdsLog{mlds.log};
-    c.ac = ac;
+    c.ac = LDPC_TILE_CONST_COEF ? kAtanhCoef : ac;
     c.k = g.k;
     c.lane = lane;
     c.wave = wave;
@@ -482,18 +488,22 @@ __global__ __launch_bounds__(64 * kTW, 1) void tile_kernel(DevGraph g, DevState 
         if (nllr && my_cnt) atomicAdd(cntl + lane, my_cnt);
         __syncthreads();
 
-        // syndrome of z (:191-204): parity of z^1 over every row
+        // syndrome of z (:191-204): row r of H_std = [A | I] has parity
+        // popcount(A_r & (z^1)_A) + (z^1)_{k+r}; A_r bit-packed (g.a_packed,
+        // scalar loads), this lane's (z^1)_A words in registers.
         uint32_t acc = 0u;
-        for (int r = wave; r < m; r += kTW) {
-            const int b = row_ptr[r], e1 = row_ptr[r + 1];
-            uint32_t par = 0u;
-            for (int e = b; e < e1; ++e) {  // zb and ib are one array: [kw + mw][64]
-                const int col = col_idx[e];
-                const int q = col < g.k ? col : col - g.k;
-                const int w = (q >> 5) + (col < g.k ? 0 : kw);
-                par ^= zb[w * kTile + lane] >> (q & 31);
+        {
+            uint32_t zr[kTKW];
+#pragma unroll
+            for (int w = 0; w < kTKW; ++w) zr[w] = w < kw ? zb[w * kTile + lane] : 0u;
+            for (int r = wave; r < m; r += kTW) {
+                const uint32_t *ar = g.a_packed + (size_t)r * kw;
+                uint32_t par = ib[(r >> 5) * kTile + lane] >> (r & 31);
+#pragma unroll
+                for (int w = 0; w < kTKW; ++w)
+                    if (w < kw) par += __builtin_popcount(ar[w] & zr[w]);
+                acc |= par & 1u;
             }
-            acc |= par & 1u;
         }
         if (acc) atomicOr((uint32_t *)bad + lane, 1u);
         __syncthreads();
@@ -539,7 +549,7 @@ __global__ __launch_bounds__(64 * kTW, 1) void tile_kernel(DevGraph g, DevState 
 }  // namespace
 
 size_t tile_lds_bytes(const DevGraph &g) {
-    if (!g.std_form || g.k <= 0 || g.max_row_deg > kTW * kTK) return 0;
+    if (!g.std_form || !g.a_packed || g.k <= 0 || g.k > 32 * kTKW || g.max_row_deg > kTW * kTK) return 0;
     const size_t b = tile_layout(g.k, g.m).total;
     return b <= kTileLdsMax ? b : 0;
 }
