@@ -60,9 +60,19 @@
 namespace ldpc {
 namespace {
 
-constexpr int kTW = 16;  // wavefronts per workgroup
-constexpr int kTK = 12;  // edges per wavefront chunk: row degree <= kTW * kTK = 192
-constexpr int kTR = 2;   // chain slots (see the ordering argument above)
+#ifndef LDPC_TILE_WAVES
+#define LDPC_TILE_WAVES 16
+#endif
+constexpr int kTW = LDPC_TILE_WAVES;  // wavefronts per workgroup
+constexpr int kTK = 192 / kTW;        // edges per wavefront chunk: row degree <= kTW * kTK = 192
+// LDPC_TILE_HOPFIRST 1: body(r) = hop(r), P3(r-1), P1(r+1) (the chain of row r
+// starts before this wavefront's P3 of row r-1; S order then needs the P3
+// completion count, and chain slots are reused every 4 rows); 0: P3(r-1),
+// hop(r), P1(r+1) (the ordering argument above, 2 slots).
+#ifndef LDPC_TILE_HOPFIRST
+#define LDPC_TILE_HOPFIRST 0
+#endif
+constexpr int kTR = LDPC_TILE_HOPFIRST ? 4 : 2;  // chain slots
 constexpr size_t kTileLdsMax = 163840;
 constexpr int kTKW = 10;  // (z^1)_A words per lane held in registers for the syndrome: k <= 320
 
@@ -86,8 +96,8 @@ __host__ __device__ inline TileLayout tile_layout(int k, int m) {
     o = al16(o + (size_t)((m + 31) / 32) * kTile * sizeof(uint32_t));
     t.lane_i = o;  // bad[64], nllr count[64], live[64]
     o = al16(o + 3 * kTile * sizeof(int));
-    t.flags = o;  // chain flag[kTR], tiny[kTR], tiny sequence, tile running
-    o = al16(o + (2 * kTR + 2) * sizeof(int));
+    t.flags = o;  // chain flag[kTR], tiny[kTR], tiny sequence, tile running, P3 counts[4]
+    o = al16(o + (2 * kTR + 6) * sizeof(int));
     t.total = o;
     return t;
 }
@@ -118,6 +128,12 @@ __device__ __forceinline__ void wait_flag(const int *p, int v) {
         if (LDPC_TILE_SLEEP) __builtin_amdgcn_s_sleep(1);
     }
 #endif
+    lds_acquire();
+}
+__device__ __forceinline__ void wait_ge(const int *p, int v) {
+    while (uniform(lds_ld(p)) < v) {
+        if (LDPC_TILE_SLEEP) __builtin_amdgcn_s_sleep(1);
+    }
     lds_acquire();
 }
 // Load through L2 (not this CU's L1): data another wavefront of the workgroup
@@ -157,6 +173,11 @@ __device__ __forceinline__ double ld_l2(const double *p) {
 #ifndef LDPC_TILE_SMALLQ
 #define LDPC_TILE_SMALLQ 0
 #endif
+//   LDPC_TILE_GROUP     edges per straight-line group in the P1 / P3 math
+#ifndef LDPC_TILE_GROUP
+#define LDPC_TILE_GROUP 1
+#endif
+constexpr int kTG = LDPC_TILE_GROUP;
 //   LDPC_TILE_CONST_COEF 1: atanh coefficients as compile-time constants
 //                       instead of kernel-argument SGPRs
 #ifndef LDPC_TILE_CONST_COEF
@@ -197,7 +218,7 @@ struct TileCtx {
     double *S;         // LDS [k][64]
     double *slot;      // LDS [kTR][64]
     uint32_t *ib;      // LDS [mw][64] z^1 of the identity columns
-    int *flag, *tinyf, *tseq;
+    int *flag, *tinyf, *tseq, *p3n;
     LdsTanh ttab;
     LdsLog ltab;
     AtanhCoef ac;
@@ -210,15 +231,27 @@ struct TileCtx {
 
 // P1 pieces: L[col] of edge i of chunk rc, E_old, and t = tanh((L - E_old)/2).
 // Loads are unconditional (index clamped into the chunk).
+// LDPC_TILE_DIAG_NOLOAD_L / _E (diagnostic builds, WRONG results): replace the
+// posterior gather / the E_old stream by a register value to time the rest.
 __device__ __forceinline__ double tile_load_l(const TileCtx &c, const RowChunk &rc, int i) {
+#ifdef LDPC_TILE_DIAG_NOLOAD_L
+    return 3.0 + (double)(int)(c.lane + i) * 0.0078125;  // |M| stays away from 0 (no rare rows)
+#endif
     const double *Ls = c.first ? c.Cb : c.Lb;
     return ld_l2(at(Ls, c.col_idx[rc.c0 + min(i, rc.cnt - 1)], c.lane));
 }
 __device__ __forceinline__ double tile_load_e(const TileCtx &c, const RowChunk &rc, int i) {
+#ifdef LDPC_TILE_DIAG_NOLOAD_E
+    return (double)(int)(c.lane + i) * 0.0625;
+#endif
     return c.first ? 0.0 : *at(c.Eb, rc.c0 + min(i, rc.cnt - 1), c.lane);
 }
 __device__ __forceinline__ bool tile_t(const TileCtx &c, double &t, double eo) {
     const double M = c.first ? t : t - eo;  // :85-90 / :260-268
+#ifdef LDPC_TILE_DIAG_NOTANH  // diagnostic (WRONG results): tanh as one fma
+    t = __builtin_fma(M, 0.125, 0.25);
+    return false;
+#endif
     if (LDPC_TILE_TANH_BF) {
         const double d = M * 0.5;
         const double r = np_tanh(d, c.ttab);
@@ -239,13 +272,26 @@ __device__ __forceinline__ bool tile_p1(const TileCtx &c, const RowChunk &rc, do
         for (int h = 0; h < LDPC_TILE_STAGES; ++h) {
             double eo[H];
 #pragma unroll
-            for (int i = h * H; i < min((h + 1) * H, kTK); ++i) {
-                t[i] = tile_load_l(c, rc, i);
-                eo[i - h * H] = tile_load_e(c, rc, i);
-            }
+            for (int g0 = h * H; g0 < min((h + 1) * H, kTK); g0 += kTG) {
+                if (g0 < rc.cnt) {
 #pragma unroll
-            for (int i = h * H; i < min((h + 1) * H, kTK); ++i)
-                if (i < rc.cnt) tiny |= tile_t(c, t[i], eo[i - h * H]);
+                    for (int i = g0; i < min(g0 + kTG, min((h + 1) * H, kTK)); ++i) {
+                        t[i] = tile_load_l(c, rc, i);
+                        eo[i - h * H] = tile_load_e(c, rc, i);
+                    }
+                }
+            }
+            // edges in groups of kTG as straight-line code (independent
+            // dependency chains the scheduler can interleave); a group's slots
+            // past the chunk hold the clamped last edge and are never used
+#pragma unroll
+            for (int g0 = h * H; g0 < min((h + 1) * H, kTK); g0 += kTG) {
+                if (g0 < rc.cnt) {
+#pragma unroll
+                    for (int i = g0; i < min(g0 + kTG, min((h + 1) * H, kTK)); ++i)
+                        tiny |= tile_t(c, t[i], eo[i - h * H]);
+                }
+            }
         }
     }
     return __ballot(tiny) != 0ull;
@@ -301,11 +347,17 @@ __device__ __forceinline__ void tile_p3(TileCtx &c, int r, double (&t)[kTK], con
 #pragma unroll
         for (int i = 0; i < kTK; ++i) eo[i] = tile_load_e(c, rc1, i);
     }
+    // hop-first order: S additions of row r wait for every wavefront's P3 of
+    // row r-1 (per-slot completion counts, rows by global index g)
+    const int g = c.ep0 + r;
+    if (LDPC_TILE_HOPFIRST && g > 0) wait_ge(c.p3n + ((g - 1) & 3), kTW * (((g - 1) >> 2) + 1));
     if (rc.deg == 0) {
         if (pf) {
 #pragma unroll
             for (int i = 0; i < kTK; ++i) t[i] = tile_load_l(c, rc1, i);
         }
+        if (LDPC_TILE_HOPFIRST && c.lane == 0)
+            __hip_atomic_fetch_add(c.p3n + (g & 3), 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         return;
     }
     const int s = r & (kTR - 1);
@@ -317,16 +369,22 @@ __device__ __forceinline__ void tile_p3(TileCtx &c, int r, double (&t)[kTK], con
     if (!tiny_row && !LDPC_TILE_P3FUSED && LDPC_TILE_SMALLQ) {
         bool big = false;
 #pragma unroll
-        for (int i = 0; i < kTK; ++i) {
-            if (i < rc.cnt) {
-                t[i] = clip_cl(P / t[i]);  // q (:159-167)
-                big |= !(fabs(t[i]) < kAtanhSmall);
+        for (int g0 = 0; g0 < kTK; g0 += kTG) {
+            if (g0 < rc.cnt) {
+#pragma unroll
+                for (int i = g0; i < min(g0 + kTG, kTK); ++i) {
+                    t[i] = clip_cl(P / t[i]);  // q (:159-167)
+                    big |= !(fabs(t[i]) < kAtanhSmall) && i < rc.cnt;
+                }
             }
         }
         if (__ballot(big) == 0ull) {
 #pragma unroll
-            for (int i = 0; i < kTK; ++i)
-                if (i < rc.cnt) t[i] = 2.0 * atanh_small(t[i], c.ac);  // :168
+            for (int g0 = 0; g0 < kTK; g0 += kTG)
+                if (g0 < rc.cnt) {
+#pragma unroll
+                    for (int i = g0; i < min(g0 + kTG, kTK); ++i) t[i] = 2.0 * atanh_small(t[i], c.ac);  // :168
+                }
         } else {
 #pragma unroll
             for (int i = 0; i < kTK; ++i)
@@ -334,8 +392,17 @@ __device__ __forceinline__ void tile_p3(TileCtx &c, int r, double (&t)[kTK], con
         }
     } else if (!tiny_row && !LDPC_TILE_P3FUSED) {
 #pragma unroll
-        for (int i = 0; i < kTK; ++i)
-            if (i < rc.cnt) t[i] = 2.0 * atanh_f(clip_cl(P / t[i]), c.ltab, c.ac);  // :159-168
+        for (int g0 = 0; g0 < kTK; g0 += kTG) {
+            if (g0 < rc.cnt) {
+#pragma unroll
+                for (int i = g0; i < min(g0 + kTG, kTK); ++i)
+#ifdef LDPC_TILE_DIAG_NOP3MATH  // diagnostic (WRONG results): E = clip(P*t)
+                    t[i] = clip_cl(P * t[i]);
+#else
+                    t[i] = 2.0 * atanh_f(clip_cl(P / t[i]), c.ltab, c.ac);  // :159-168
+#endif
+            }
+        }
     } else if (tiny_row) {
         // rare: q = prod of the others, in order (np.prod(np.delete(...)), :164)
         const int pos0 = c.wave * rc.C;
@@ -388,14 +455,24 @@ __device__ __forceinline__ void tile_p3(TileCtx &c, int r, double (&t)[kTK], con
         }
         if (pf) t[i] = tile_load_l(c, rc1, i);
     }
+    if (LDPC_TILE_HOPFIRST) {
+        lds_release();  // this row's S additions before the count
+        if (c.lane == 0)
+            __hip_atomic_fetch_add(c.p3n + (g & 3), 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
 }
 
 __device__ __forceinline__ void tile_body(TileCtx &c, int r, int m, double (&tcur)[kTK], bool &ycur,
                                           double (&toth)[kTK], bool &yoth, double (&eo)[kTK]) {
     RowChunk rc1{};
     if (r + 1 < m) rc1 = chunk_of(c.row_ptr, r + 1, c.wave);
-    if (r >= 1) tile_p3(c, r - 1, toth, rc1, eo);
-    if (r < m) tile_hop(c, r, tcur, ycur);
+    if (LDPC_TILE_HOPFIRST) {
+        if (r < m) tile_hop(c, r, tcur, ycur);
+        if (r >= 1) tile_p3(c, r - 1, toth, rc1, eo);
+    } else {
+        if (r >= 1) tile_p3(c, r - 1, toth, rc1, eo);
+        if (r < m) tile_hop(c, r, tcur, ycur);
+    }
     if (r + 1 < m) {
         if (LDPC_TILE_PREFETCH && r >= 1) {
             yoth = tile_p1_math(c, rc1, toth, eo);
@@ -403,6 +480,71 @@ __device__ __forceinline__ void tile_body(TileCtx &c, int r, int m, double (&tcu
             yoth = tile_p1(c, rc1, toth);
         }
     }
+}
+
+// End of a pass, once every column's z^1 bit is in zb (A part) / ib (identity
+// part) and the normalized-LLR counts are in cntl: the syndrome (:191-204) of
+// every frame and the per-frame exits of vn_kernel (static schedule).  Row r
+// of H_std = [A | I] has parity popcount(A_r & (z^1)_A) + (z^1)_{k+r}; A_r is
+// bit-packed (g.a_packed, scalar loads), this lane's (z^1)_A words sit in
+// registers.  Returns whether any frame of the tile still runs (uniform).
+__device__ __forceinline__ bool tile_pass_end(const DevGraph &g, const DevState &st, uint32_t *zb, const uint32_t *ib,
+                                              int *bad, int *cntl, int *livel, int *running, int it, int max_iter,
+                                              int nllr, int tile, int wave, int nwaves, bool live) {
+    const int kw = (g.k + 31) >> 5, mw = (g.m + 31) >> 5;
+    const int lane = threadIdx.x & 63;
+    const int f = tile * kTile + lane;
+    uint32_t acc = 0u;
+    {
+        uint32_t zr[kTKW];
+#pragma unroll
+        for (int w = 0; w < kTKW; ++w) zr[w] = w < kw ? zb[w * kTile + lane] : 0u;
+        for (int r = wave; r < g.m; r += nwaves) {
+            const uint32_t *ar = g.a_packed + (size_t)r * kw;
+            uint32_t par = ib[(r >> 5) * kTile + lane] >> (r & 31);
+#pragma unroll
+            for (int w = 0; w < kTKW; ++w)
+                if (w < kw) par += __builtin_popcount(ar[w] & zr[w]);
+            acc |= par & 1u;
+        }
+    }
+    if (acc) atomicOr((uint32_t *)bad + lane, 1u);
+    __syncthreads();
+
+    if (wave == 0) {  // per-frame exits, as vn_kernel (static schedule)
+        bool still = false;
+        if (live) {
+            if (nllr) {
+                const int cn = cntl[lane];
+                st.nllr_cnt[f] = cn;
+                if (st.nllr_hist) st.nllr_hist[(size_t)f * st.hist_stride + it] = g.k > 0 ? (double)cn / g.k : 0.0;
+            }
+            if (bad[lane] == 0) {  // syndrome zero: Result.OK at this iteration (:231-241)
+                st.done[f] = 1;
+                st.conv[f] = it;
+                st.status[f] = 0;
+                st.iters[f] = it + 1;
+            } else if (it == max_iter - 1) {  // Result.DATA_TRANSFER_NOT_OK (:244-253)
+                st.done[f] = 1;
+                st.conv[f] = -1;
+                st.status[f] = 1;
+                st.iters[f] = it + 1;
+            } else {
+                still = true;
+            }
+        }
+        livel[lane] = still ? 1 : 0;
+        bad[lane] = 0;
+        cntl[lane] = 0;
+        const unsigned long long any = __ballot(still);
+        if (lane == 0) {
+            *running = any != 0ull ? 1 : 0;
+            if (!any) st.tile_active[tile] = 0;
+        }
+    }
+    for (int i = threadIdx.x; i < (kw + mw) * kTile; i += blockDim.x) zb[i] = 0u;  // zb and ib are adjacent
+    __syncthreads();
+    return *running != 0;
 }
 
 __global__ __launch_bounds__(64 * kTW, 1) void tile_kernel(DevGraph g, DevState st, int max_iter, int nllr,
@@ -428,6 +570,7 @@ __global__ __launch_bounds__(64 * kTW, 1) void tile_kernel(DevGraph g, DevState 
     for (int i = threadIdx.x; i < 2 * kTile; i += blockDim.x) bad[i] = 0;
     if (threadIdx.x < 2 * kTR) flags[threadIdx.x] = -1;
     if (threadIdx.x == 2 * kTR) flags[2 * kTR] = 0;
+    if (threadIdx.x >= 2 * kTR + 2 && threadIdx.x < 2 * kTR + 6) flags[threadIdx.x] = 0;
     const int lane = threadIdx.x & 63;
     const int wave = uniform(threadIdx.x >> 6);
     const int f = tile * kTile + lane;
@@ -448,6 +591,7 @@ __global__ __launch_bounds__(64 * kTW, 1) void tile_kernel(DevGraph g, DevState 
     c.flag = flags;
     c.tinyf = flags + kTR;
     c.tseq = flags + 2 * kTR;
+    c.p3n = flags + 2 * kTR + 2;
     c.ttab = LdsTanh{mlds.tanh};
     c.ltab = LdsLog{mlds.log};
     c.ac = LDPC_TILE_CONST_COEF ? kAtanhCoef : ac;
@@ -488,63 +632,12 @@ __global__ __launch_bounds__(64 * kTW, 1) void tile_kernel(DevGraph g, DevState 
         if (nllr && my_cnt) atomicAdd(cntl + lane, my_cnt);
         __syncthreads();
 
-        // syndrome of z (:191-204): row r of H_std = [A | I] has parity
-        // popcount(A_r & (z^1)_A) + (z^1)_{k+r}; A_r bit-packed (g.a_packed,
-        // scalar loads), this lane's (z^1)_A words in registers.
-        uint32_t acc = 0u;
-        {
-            uint32_t zr[kTKW];
-#pragma unroll
-            for (int w = 0; w < kTKW; ++w) zr[w] = w < kw ? zb[w * kTile + lane] : 0u;
-            for (int r = wave; r < m; r += kTW) {
-                const uint32_t *ar = g.a_packed + (size_t)r * kw;
-                uint32_t par = ib[(r >> 5) * kTile + lane] >> (r & 31);
-#pragma unroll
-                for (int w = 0; w < kTKW; ++w)
-                    if (w < kw) par += __builtin_popcount(ar[w] & zr[w]);
-                acc |= par & 1u;
-            }
-        }
-        if (acc) atomicOr((uint32_t *)bad + lane, 1u);
-        __syncthreads();
-
-        if (wave == 0) {  // per-frame exits, as vn_kernel (static schedule)
-            bool still = false;
-            if (c.live) {
-                if (nllr) {
-                    const int cn = cntl[lane];
-                    st.nllr_cnt[f] = cn;
-                    if (st.nllr_hist)
-                        st.nllr_hist[(size_t)f * st.hist_stride + it] = g.k > 0 ? (double)cn / g.k : 0.0;
-                }
-                if (bad[lane] == 0) {  // syndrome zero: Result.OK at this iteration (:231-241)
-                    st.done[f] = 1;
-                    st.conv[f] = it;
-                    st.status[f] = 0;
-                    st.iters[f] = it + 1;
-                } else if (it == max_iter - 1) {  // Result.DATA_TRANSFER_NOT_OK (:244-253)
-                    st.done[f] = 1;
-                    st.conv[f] = -1;
-                    st.status[f] = 1;
-                    st.iters[f] = it + 1;
-                } else {
-                    still = true;
-                }
-            }
-            livel[lane] = still ? 1 : 0;
-            bad[lane] = 0;
-            cntl[lane] = 0;
-            const unsigned long long any = __ballot(still);
-            if (lane == 0) {
-                flags[2 * kTR + 1] = any != 0ull ? 1 : 0;
-                if (!any) st.tile_active[tile] = 0;
-            }
-        }
-        for (int i = threadIdx.x; i < (kw + mw) * kTile; i += blockDim.x) zb[i] = 0u;
-        __syncthreads();
-        if (!flags[2 * kTR + 1]) break;
+        if (!tile_pass_end(g, st, zb, ib, bad, cntl, livel, flags + 2 * kTR + 1, it, max_iter, nllr, tile, wave,
+                           kTW, c.live))
+            break;
     }
 }
+
 
 }  // namespace
 
