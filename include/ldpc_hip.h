@@ -90,12 +90,16 @@ int ldpc_graph_destroy(ldpc_graph *g);
  * "cn_kernel": one wavefront per row, 24 B/edge) -- measurement labels. */
 const char *ldpc_cn_kernel_name(const ldpc_graph *g);
 /* LDS bytes per workgroup of the tile-resident decoder for this graph, or 0 if
- * it does not apply (it needs H_std = [A | I_m], row degree <= 192 and the A
- * column sums of 64 frames in LDS: k*512 B + ~13 KB <= 160 KB, e.g.
- * wimax_576_0.5).  Where it applies, ldpc_decode_f64 and the static schedule of
- * ldpc_mc_run decode a whole chunk in ONE launch (tile_kernels.hip); the
+ * it does not apply.  It needs H_std = [A | I_m] and the A column sums of the
+ * workgroup's frames in LDS: 64 frames (tile_kernels.hip: k*512 B + ~13 KB <=
+ * 160 KB, row degree <= 192, e.g. wimax_576_0.5), else 16 or 8 frames
+ * (tile_sub.hip: the WiMAX 2304 codes).  Where it applies, ldpc_decode_f64 and
+ * the static schedule of ldpc_mc_run decode a whole chunk in ONE launch; the
  * separate per-iteration launches remain available via LDPC_F_SPLIT. */
 int64_t ldpc_tile_lds_bytes(const ldpc_graph *g);
+/* "tile_kernel" (64 frames per workgroup), "tile_sub_kernel" (16 or 8), or ""
+ * when the tile-resident decoder does not apply -- measurement label. */
+const char *ldpc_tile_kernel_name(const ldpc_graph *g);
 /* Physical-mode kernel for this (sparse) graph: "phys_reg_kernel" / "phys_kernel"
  * (state in LDS) or "phys_cn_tile_kernel" (state in HBM). */
 const char *ldpc_phys_kernel_name(const ldpc_graph *g, uint32_t flags);

@@ -216,6 +216,9 @@ hipError_t run_iterations(ldpc_decoder *d, const DevGraph &G, const DevState &st
     DevState st = st_in;
     if (!split && ldpc::use_tile(G) && st.ntiles <= st.nslots)  // one launch: every tile runs to its own exit
         return timed(d, LDPC_K_TILE, s, [&] { return ldpc::launch_tile(G, st, max_iter, nllr, s); });
+    // cn_rare_kernel clears the OTHER parity's count for the next CN; the one
+    // the last iteration used (or an early stop left) is cleared here
+    if ((e = hipMemsetAsync(st.rare_count, 0, sizeof(int) * 2, s))) return e;
     if (poll) {
         if (d->pactive_cap < max_iter) {
             (void)hipFree(d->pactive);
@@ -402,6 +405,11 @@ int ldpc_graph_destroy(ldpc_graph *g) {
 const char *ldpc_cn_kernel_name(const ldpc_graph *g) {
     if (!g) return "";
     return ldpc::use_cn_row(g->dg) ? "cn_row_kernel" : "cn_kernel";
+}
+
+const char *ldpc_tile_kernel_name(const ldpc_graph *g) {
+    if (!g || !ldpc::use_tile(g->dg)) return "";
+    return ldpc::tile_kernel_name(g->dg);
 }
 
 int64_t ldpc_tile_lds_bytes(const ldpc_graph *g) {
@@ -696,6 +704,7 @@ int mc_stream_point(ldpc_decoder *d, uint64_t seed, int p, double sigma, int64_t
                      [&] { return ldpc::launch_refill(G, st, seed, p, sigma, frame0, total, next, s); });
     };
     HIP_TRY(refill());
+    HIP_TRY(hipMemsetAsync(st.rare_count, 0, sizeof(int) * 2, s));  // see run_iterations
     const int64_t slots = (int64_t)ntiles * kTile;
     const int64_t min_steps = (total + slots - 1) / slots;            // every slot needs >= 1 step per frame
     const int64_t max_steps = (min_steps + 1) * (int64_t)max_iter;   // every frame stops by max_iter

@@ -74,9 +74,15 @@ hipError_t launch_vn(const DevGraph &g, const DevState &st, int it, int max_iter
 // tile-resident decoder (tile_kernels.hip): all iterations of a tile in one
 // workgroup, check- and variable-node updates fused; [A | I_m] graphs whose A
 // column sums fit in LDS (tile_lds_bytes > 0).  Needs st.ntiles <= st.nslots.
+// Codes whose column sums of 64 frames do not fit (the WiMAX 2304 codes) run
+// the sub-tile decoder (tile_sub.hip: 16 or 8 frames per workgroup).
 size_t tile_lds_bytes(const DevGraph &g);
+const char *tile_kernel_name(const DevGraph &g);  // "tile_kernel", "tile_sub_kernel" or ""
 bool use_tile(const DevGraph &g);
 hipError_t launch_tile(const DevGraph &g, const DevState &st, int max_iter, bool nllr, hipStream_t s);
+int sub_frames(const DevGraph &g);
+size_t sub_lds_bytes(const DevGraph &g);
+hipError_t launch_tile_sub(const DevGraph &g, const DevState &st, int max_iter, bool nllr, hipStream_t s);
 hipError_t launch_stream_init(const DevGraph &g, const DevState &st, hipStream_t s);
 hipError_t launch_refill(const DevGraph &g, const DevState &st, uint64_t seed, int snr_point, double sigma,
                          int64_t frame0, int64_t total, unsigned long long *next, hipStream_t s);

@@ -1,0 +1,59 @@
+// tile_common.h -- synchronisation helpers shared by the tile-resident parity
+// decoders (tile_kernels.hip: 64 frames per workgroup; tile_sub.hip: 16 or 8).
+// Wavefronts of one workgroup hand the check-row product along through LDS
+// words guarded by flags (no workgroup barrier on the chain).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstddef>
+
+#include "cn_common.h"
+
+namespace ldpc {
+namespace {
+
+__host__ __device__ inline size_t al16(size_t x) { return (x + 15) & ~(size_t)15; }
+
+__device__ __forceinline__ int lds_ld(const int *p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void lds_st(int *p, int v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+// LDS-only fences: order this wavefront's LDS accesses around a flag without
+// waiting for its outstanding global stores.
+__device__ __forceinline__ void lds_release() { __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local"); }
+__device__ __forceinline__ void lds_acquire() { __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local"); }
+// Compile-time knobs (A/B builds only): LDPC_TILE_SLEEP polls with s_sleep 1
+// between flag reads; LDPC_TILE_PRIO raises the wavefront's issue priority
+// while it carries the product chain; LDPC_TILE_DIAG_NOCHAIN (diagnostic,
+// WRONG results) skips every wait to time the pipeline without the chain.
+#ifndef LDPC_TILE_SLEEP
+#define LDPC_TILE_SLEEP 1
+#endif
+#ifndef LDPC_TILE_PRIO
+#define LDPC_TILE_PRIO 0
+#endif
+__device__ __forceinline__ void wait_flag(const int *p, int v) {
+#ifndef LDPC_TILE_DIAG_NOCHAIN
+    while (uniform(lds_ld(p)) != v) {
+        if (LDPC_TILE_SLEEP) __builtin_amdgcn_s_sleep(1);
+    }
+#endif
+    lds_acquire();
+}
+__device__ __forceinline__ void wait_ge(const int *p, int v) {
+    while (uniform(lds_ld(p)) < v) {
+        if (LDPC_TILE_SLEEP) __builtin_amdgcn_s_sleep(1);
+    }
+    lds_acquire();
+}
+// Load through L2 (not this CU's L1): data another wavefront of the workgroup
+// stored (posteriors, rare-row scratch).
+__device__ __forceinline__ double ld_l2(const double *p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+
+}  // namespace
+}  // namespace ldpc

@@ -54,6 +54,7 @@
 #include <cstdlib>
 
 #include "cn_common.h"
+#include "tile_common.h"
 #include "spa_device.h"
 #include "spa_math.h"
 
@@ -80,7 +81,6 @@ constexpr int kTKW = 10;  // (z^1)_A words per lane held in registers for the sy
 struct TileLayout {
     size_t S, math, slot, zb, ib, lane_i, flags, total;
 };
-__host__ __device__ inline size_t al16(size_t x) { return (x + 15) & ~(size_t)15; }
 __host__ __device__ inline TileLayout tile_layout(int k, int m) {
     TileLayout t;
     size_t o = 0;
@@ -100,46 +100,6 @@ __host__ __device__ inline TileLayout tile_layout(int k, int m) {
     o = al16(o + (2 * kTR + 6) * sizeof(int));
     t.total = o;
     return t;
-}
-
-__device__ __forceinline__ int lds_ld(const int *p) {
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-__device__ __forceinline__ void lds_st(int *p, int v) {
-    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-// LDS-only fences: order this wavefront's LDS accesses around a flag without
-// waiting for its outstanding global stores.
-__device__ __forceinline__ void lds_release() { __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local"); }
-__device__ __forceinline__ void lds_acquire() { __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local"); }
-// Compile-time knobs (A/B builds only): LDPC_TILE_SLEEP polls with s_sleep 1
-// between flag reads; LDPC_TILE_PRIO raises the wavefront's issue priority
-// while it carries the product chain; LDPC_TILE_DIAG_NOCHAIN (diagnostic,
-// WRONG results) skips every wait to time the pipeline without the chain.
-#ifndef LDPC_TILE_SLEEP
-#define LDPC_TILE_SLEEP 1
-#endif
-#ifndef LDPC_TILE_PRIO
-#define LDPC_TILE_PRIO 0
-#endif
-__device__ __forceinline__ void wait_flag(const int *p, int v) {
-#ifndef LDPC_TILE_DIAG_NOCHAIN
-    while (uniform(lds_ld(p)) != v) {
-        if (LDPC_TILE_SLEEP) __builtin_amdgcn_s_sleep(1);
-    }
-#endif
-    lds_acquire();
-}
-__device__ __forceinline__ void wait_ge(const int *p, int v) {
-    while (uniform(lds_ld(p)) < v) {
-        if (LDPC_TILE_SLEEP) __builtin_amdgcn_s_sleep(1);
-    }
-    lds_acquire();
-}
-// Load through L2 (not this CU's L1): data another wavefront of the workgroup
-// stored (posteriors, rare-row scratch).
-__device__ __forceinline__ double ld_l2(const double *p) {
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // Compile-time layout/schedule switches (A/B builds; defaults = measured best):
@@ -641,10 +601,31 @@ __global__ __launch_bounds__(64 * kTW, 1) void tile_kernel(DevGraph g, DevState 
 
 }  // namespace
 
-size_t tile_lds_bytes(const DevGraph &g) {
+size_t tile64_lds_bytes(const DevGraph &g) {
     if (!g.std_form || !g.a_packed || g.k <= 0 || g.k > 32 * kTKW || g.max_row_deg > kTW * kTK) return 0;
     const size_t b = tile_layout(g.k, g.m).total;
     return b <= kTileLdsMax ? b : 0;
+}
+
+// LDPC_TILE_SUB=0 keeps the long codes on the separate CN/VN launches (A/B)
+static bool sub_enabled() {
+    static const int force = [] {
+        const char *e = getenv("LDPC_TILE_SUB");
+        return e ? atoi(e) : -1;
+    }();
+    return force != 0;
+}
+
+size_t tile_lds_bytes(const DevGraph &g) {
+    const size_t b = tile64_lds_bytes(g);
+    if (b) return b;
+    return sub_enabled() ? sub_lds_bytes(g) : 0;
+}
+
+const char *tile_kernel_name(const DevGraph &g) {
+    if (tile64_lds_bytes(g)) return "tile_kernel";
+    if (sub_enabled() && sub_lds_bytes(g)) return "tile_sub_kernel";
+    return "";
 }
 
 // LDPC_TILE=0 forces the separate CN/VN launches (A/B, tests)
@@ -657,8 +638,9 @@ bool use_tile(const DevGraph &g) {
 }
 
 hipError_t launch_tile(const DevGraph &g, const DevState &st, int max_iter, bool nllr, hipStream_t s) {
-    const size_t lds = tile_lds_bytes(g);
-    if (!lds || st.ntiles > st.nslots) return hipErrorInvalidValue;
+    if (st.ntiles > st.nslots) return hipErrorInvalidValue;
+    const size_t lds = tile64_lds_bytes(g);
+    if (!lds) return sub_enabled() ? launch_tile_sub(g, st, max_iter, nllr, s) : hipErrorInvalidValue;
     tile_kernel<<<st.ntiles, 64 * kTW, lds, s>>>(g, st, max_iter, nllr ? 1 : 0, g.col_idx, g.row_ptr, kAtanhCoef);
     return hipGetLastError();
 }

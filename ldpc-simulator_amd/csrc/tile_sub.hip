@@ -1,0 +1,488 @@
+// tile_sub.hip -- the tile-resident parity decoder for long codes (gfx950).
+//
+// tile_kernels.hip decodes 64 frames per workgroup with the column sums
+// S_j = ((0 + E_r0j) + E_r1j) + ... (rows ascending: scipy csr_matvec of E^T,
+// the reference's rounding order, python_ldpc_app/spa_decoder.py:173-185)
+// kept in LDS: k x 64 x 8 B, which holds only for k <= ~300.  The WiMAX 2304
+// codes (k = 1152, 1728) fit when a workgroup decodes a SUB-tile of F = 16 or
+// 8 frames (S = k x F x 8 B: 147 KB / 110 KB).  A wavefront instruction then
+// covers Q = 64/F edges of F frames: lane = j*F + f (lane group j, frame f).
+//
+// Row r's edges are split into 16 contiguous wavefront chunks as in
+// tile_kernel (wavefront w: positions [w*C, w*C + C), C = ceil(deg/16)), and a
+// chunk into Q contiguous lane-group pieces of CS = ceil(C/Q) edges: lane group
+// j holds positions j*CS .. j*CS + CS - 1 of the chunk in register slots
+// 0..CS-1.  The left-to-right product P = t0 * t1 * ... (:151-152) crosses lane
+// groups inside the wavefront: starting from the prefix P of the wavefront
+// before it, every lane multiplies its own slots in order; lane group j's
+// result is the prefix through group j, broadcast to all lanes (ds_bpermute)
+// before group j+1's turn.  Groups with no edges are skipped.  The rest is
+// tile_kernel's pipeline and ordering argument unchanged:
+//
+//   body(r):  P3(r-1)  E_new = 2 atanh(clip(P/t)) (:159-168), stored, added
+//                      into S (LDS, per lane: column of its edge, its frame);
+//             hop(r)   this wavefront's piece of row r's product;
+//             P1(r+1)  L[col], E_old, t = tanh((L - E_old)/2) (:138-146,
+//                      :260-268).
+//
+// Per edge and iteration the HBM traffic is the algorithmic 16 B (E_old read,
+// E_new write) plus the L[col] gather (8 B, L2/MALL): the split CN/VN
+// launches this replaces move 24 + 8 B plus the gathers.  The identity column
+// k+r of a [A | I] graph has row r's last edge only; its posterior
+// ch + (0 + E) is final when row r is.
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstdlib>
+
+#include "cn_common.h"
+#include "spa_device.h"
+#include "spa_math.h"
+#include "tile_common.h"
+
+namespace ldpc {
+namespace {
+
+constexpr int kSW = 16;                 // wavefronts per workgroup
+constexpr size_t kSubLdsMax = 163840;
+
+template <int Q>
+struct SubCfg {
+    static constexpr int F = kTile / Q;           // frames per workgroup
+    static constexpr int K = Q == 4 ? 10 : 8;     // slots per lane: row degree <= kSW * Q * K
+};
+
+struct SubLayout {
+    size_t S, math, slot, zb, ib, lane_i, flags, dummy, total;
+};
+__host__ __device__ inline SubLayout sub_layout(int k, int m, int F) {
+    SubLayout t;
+    size_t o = 0;
+    t.S = o;  // [k][F] column sums
+    o = al16(o + (size_t)k * F * sizeof(double));
+    t.math = o;
+    o = al16(o + sizeof(MathLds));
+    t.slot = o;  // [2][F] chain slots
+    o = al16(o + 2 * (size_t)F * sizeof(double));
+    t.zb = o;  // [kw][F] z^1 bits of the A columns
+    o = al16(o + (size_t)((k + 31) / 32) * F * sizeof(uint32_t));
+    t.ib = o;  // [mw][F] z^1 bits of the identity columns (adjacent to zb)
+    o = al16(o + (size_t)((m + 31) / 32) * F * sizeof(uint32_t));
+    t.lane_i = o;  // bad[F], nllr count[F], live[F]
+    o = al16(o + 3 * (size_t)F * sizeof(int));
+    t.flags = o;  // chain flag[2], tiny[2], tiny sequence, running
+    o = al16(o + 6 * sizeof(int));
+    t.dummy = o;  // [F] target of the identity lane's masked-off S update
+    o = al16(o + (size_t)F * sizeof(double));
+    t.total = o;
+    return t;
+}
+
+struct SubChunk {
+    int deg, c0, cnt, CS;
+};
+__device__ __forceinline__ SubChunk sub_chunk(const int *__restrict__ row_ptr, int r, int wave, int Q) {
+    SubChunk c;
+    const int beg = row_ptr[r];
+    c.deg = row_ptr[r + 1] - beg;
+    const int C = (c.deg + kSW - 1) / kSW;
+    c.c0 = beg + wave * C;
+    c.cnt = max(0, min(c.deg - wave * C, C));
+    c.CS = (C + Q - 1) / Q;
+    return c;
+}
+
+template <int Q>
+struct SubCtx {
+    static constexpr int F = SubCfg<Q>::F;
+    static constexpr int K = SubCfg<Q>::K;
+    const int *__restrict__ col_idx;
+    const int *__restrict__ row_ptr;
+    // per-lane bases: element (item) of this lane's frame at [item * 64]
+    double *Eb;
+    double *Lb;
+    const double *Cb;
+    double *Tb;     // rare-row scratch of this workgroup, element (pos) at [pos * F]
+    double *S;      // LDS, element (col) at [col * F]
+    double *dummy;  // LDS, this lane's frame
+    double *slot;   // LDS, chain slot s at [s * F]
+    uint32_t *ib;   // LDS, word w at [w * F]
+    int *flag, *tinyf, *tseq;
+    LdsTanh ttab;
+    LdsLog ltab;
+    AtanhCoef ac;
+    int k, wave, j, f;
+    int ep0;
+    bool first, live;
+    int ntiny;
+};
+
+// this lane's edge count in chunk rc, and the edge of its slot i (clamped
+// into the chunk: slots past the piece load the chunk's last edge again)
+template <int Q>
+__device__ __forceinline__ int sub_nj(const SubCtx<Q> &c, const SubChunk &rc) {
+    return max(0, min(rc.cnt - c.j * rc.CS, rc.CS));
+}
+template <int Q>
+__device__ __forceinline__ int sub_edge(const SubCtx<Q> &c, const SubChunk &rc, int i) {
+    return rc.c0 + min(c.j * rc.CS + i, rc.cnt - 1);
+}
+
+// P1: t = tanh((L[col] - E_old)/2) for this lane's slots; returns whether
+// some lane's own edge has |t| <= 1e-10 (:159).
+template <int Q>
+__device__ __forceinline__ bool sub_p1(const SubCtx<Q> &c, const SubChunk &rc, double (&t)[SubCfg<Q>::K]) {
+    constexpr int K = SubCfg<Q>::K;
+    bool tiny = false;
+    if (rc.cnt > 0) {
+        const int nj = sub_nj(c, rc);
+        int col[K];
+#pragma unroll
+        for (int i = 0; i < K; ++i)
+            if (i < rc.CS) col[i] = c.col_idx[sub_edge(c, rc, i)];
+        double eo[K];
+#pragma unroll
+        for (int i = 0; i < K; ++i) {
+            if (i < rc.CS) {
+                t[i] = c.first ? c.Cb[(size_t)col[i] * kTile] : ld_l2(c.Lb + (size_t)col[i] * kTile);
+                eo[i] = c.first ? 0.0 : c.Eb[(size_t)sub_edge(c, rc, i) * kTile];
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < K; ++i) {
+            if (i < rc.CS) {
+                const double M = c.first ? t[i] : t[i] - eo[i];  // :85-90 / :260-268
+                const double d = M * 0.5;
+                const double r = np_tanh(d, c.ttab);
+                t[i] = d > 17.5 ? kCL : (d < -17.5 ? -kCL : r);  // :138-146
+                tiny |= i < nj && !(fabs(t[i]) > kTiny);
+            }
+        }
+    }
+    return __ballot(tiny) != 0ull;
+}
+
+__device__ __forceinline__ double shfl_d(double v, int src) {
+    const uint64_t u = dbits(v);
+    const int lo = __shfl((int)(uint32_t)u, src, 64);
+    const int hi = __shfl((int)(uint32_t)(u >> 32), src, 64);
+    return dfrom(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
+}
+
+// hop: this wavefront's chunk of row r's left-to-right product.
+template <int Q>
+__device__ __forceinline__ void sub_hop(const SubCtx<Q> &c, int r, const double (&t)[SubCfg<Q>::K], bool tiny) {
+    constexpr int F = SubCfg<Q>::F, K = SubCfg<Q>::K;
+    const SubChunk rc = sub_chunk(c.row_ptr, r, c.wave, Q);
+    if (rc.deg == 0) return;  // spa_decoder.py:115-122
+    const int s = r & 1;
+    const int ep = ((c.ep0 + r) & 0x3ffffff) * 32;
+    double *sl = c.slot + s * F;
+    double P = 1.0;  // 1.0 * t0 == t0 exactly
+    if (c.wave != 0) {
+        wait_flag(c.flag + s, ep + c.wave);
+        P = *sl;
+    }
+    const int nj = sub_nj(c, rc);
+#pragma unroll
+    for (int jj = 0; jj < Q; ++jj) {
+        if (jj * rc.CS < rc.cnt) {  // lane group jj holds edges of this chunk
+            double Pl = P;
+#pragma unroll
+            for (int i = 0; i < K; ++i)
+                if (i < rc.CS) Pl = i < nj ? Pl * t[i] : Pl;
+            P = shfl_d(Pl, jj * F + c.f);
+        }
+    }
+    if ((threadIdx.x & 63) == 0) {
+        if (c.wave == 0)
+            lds_st(c.tinyf + s, tiny ? 1 : 0);
+        else if (tiny)
+            lds_st(c.tinyf + s, 1);
+    }
+    if (c.j == 0) *sl = P;
+    lds_release();
+    if ((threadIdx.x & 63) == 0) lds_st(c.flag + s, ep + c.wave + 1);
+}
+
+// P3: E_new of this lane's slots of row r, stored and folded into S; the
+// identity column's posterior and z^1 bit.
+template <int Q>
+__device__ __forceinline__ void sub_p3(SubCtx<Q> &c, int r, double (&t)[SubCfg<Q>::K]) {
+    constexpr int F = SubCfg<Q>::F, K = SubCfg<Q>::K;
+    const SubChunk rc = sub_chunk(c.row_ptr, r, c.wave, Q);
+    if (rc.deg == 0) return;
+    const int s = r & 1;
+    const int ep = ((c.ep0 + r) & 0x3ffffff) * 32;
+    wait_flag(c.flag + s, ep + kSW);
+    const bool tiny_row = uniform(lds_ld(c.tinyf + s)) != 0;
+    if (rc.cnt == 0) {  // no edges here (short rows): still take part in a rare row's parking count
+        if (tiny_row) {
+            c.ntiny += 1;
+            if ((threadIdx.x & 63) == 0)
+                __hip_atomic_fetch_add(c.tseq, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+            wait_flag(c.tseq, c.ntiny * kSW);
+        }
+        return;
+    }
+    const double P = c.slot[s * F];
+    const int nj = sub_nj(c, rc);
+    int col[K];
+#pragma unroll
+    for (int i = 0; i < K; ++i)
+        if (i < rc.CS) col[i] = c.col_idx[sub_edge(c, rc, i)];
+    if (!tiny_row) {
+#pragma unroll
+        for (int i = 0; i < K; ++i)
+            if (i < rc.CS) t[i] = 2.0 * atanh_f(clip_cl(P / t[i]), c.ltab, c.ac);  // :159-168
+    } else {
+        // rare: q = in-order product of the others (np.prod(np.delete(...)),
+        // :164) for an edge with |t| <= 1e-10; t parked at row positions
+        const int rb = c.row_ptr[r];
+#pragma unroll
+        for (int i = 0; i < K; ++i)
+            if (i < rc.CS && i < nj) c.Tb[(size_t)(sub_edge(c, rc, i) - rb) * F] = t[i];
+        __builtin_amdgcn_s_waitcnt(0);  // scratch stores have reached L2
+        c.ntiny += 1;
+        if ((threadIdx.x & 63) == 0) __hip_atomic_fetch_add(c.tseq, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        wait_flag(c.tseq, c.ntiny * kSW);
+#pragma unroll
+        for (int i = 0; i < K; ++i) {
+            if (i < rc.CS) {
+                const double ti = t[i];
+                double q;
+                if (fabs(ti) > kTiny || i >= nj) {
+                    q = P / ti;
+                } else {
+                    const int pos = sub_edge(c, rc, i) - rb;
+                    q = 1.0;
+                    bool fst = true;
+                    for (int p = 0; p < rc.deg; ++p) {
+                        if (p == pos) continue;
+                        const double t2 = ld_l2(c.Tb + (size_t)p * F);
+                        q = fst ? t2 : q * t2;
+                        fst = false;
+                    }
+                }
+                t[i] = 2.0 * atanh_f(clip_cl(q), c.ltab, c.ac);
+            }
+        }
+    }
+    if (c.live) {
+#pragma unroll
+        for (int i = 0; i < K; ++i)
+            if (i < rc.CS && i < nj) c.Eb[(size_t)sub_edge(c, rc, i) * kTile] = t[i];
+    }
+    // S_col += E_new, rows ascending (a column occurs once per row: no two
+    // lanes of a row share (col, frame)); the identity edge goes to `dummy`
+    double EnI = 0.0;
+    int colI = -1;
+#pragma unroll
+    for (int i = 0; i < K; ++i) {
+        if (i < rc.CS) {
+            const bool own = i < nj;
+            const bool a = own && col[i] < c.k;
+            double *sp = a ? c.S + (size_t)col[i] * F : c.dummy;
+            *sp = *sp + t[i];
+            if (own && !a) {
+                EnI = t[i];
+                colI = col[i];
+            }
+        }
+    }
+    if (colI >= 0) {  // identity column: L = ch + (0 + E) (:173-185)
+        const double Lj = c.Cb[(size_t)colI * kTile] + (0.0 + EnI);
+        if (c.live) c.Lb[(size_t)colI * kTile] = Lj;
+        if (!(Lj < 0.0)) {
+            const int q = colI - c.k;
+            atomicOr(c.ib + (q >> 5) * F, 1u << (q & 31));
+        }
+    }
+}
+
+template <int Q>
+__device__ __forceinline__ void sub_body(SubCtx<Q> &c, int r, int m, double (&tcur)[SubCfg<Q>::K], bool ycur,
+                                         double (&toth)[SubCfg<Q>::K], bool &yoth) {
+    if (r >= 1) sub_p3(c, r - 1, toth);
+    if (r < m) sub_hop(c, r, tcur, ycur);
+    if (r + 1 < m) yoth = sub_p1(c, sub_chunk(c.row_ptr, r + 1, c.wave, Q), toth);
+}
+
+template <int Q>
+__global__ __launch_bounds__(64 * kSW, 1) void tile_sub_kernel(DevGraph g, DevState st, int max_iter, int nllr,
+                                                               const int *__restrict__ col_idx,
+                                                               const int *__restrict__ row_ptr, AtanhCoef ac) {
+    constexpr int F = SubCfg<Q>::F, K = SubCfg<Q>::K;
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+    const SubLayout ly = sub_layout(g.k, g.m, F);
+    double *S = (double *)(lds + ly.S);
+    MathLds &mlds = *(MathLds *)(lds + ly.math);
+    uint32_t *zb = (uint32_t *)(lds + ly.zb);
+    uint32_t *ib = (uint32_t *)(lds + ly.ib);
+    int *bad = (int *)(lds + ly.lane_i);
+    int *cntl = bad + F;
+    int *livel = cntl + F;
+    int *flags = (int *)(lds + ly.flags);
+    const int kw = (g.k + 31) >> 5, mw = (g.m + 31) >> 5;
+    const int tile = blockIdx.x / Q, sub = blockIdx.x % Q;
+    if (tile >= st.ntiles) return;  // block-uniform
+
+    fill_math_lds(mlds);
+    for (int i = threadIdx.x; i < g.k * F; i += blockDim.x) S[i] = 0.0;
+    for (int i = threadIdx.x; i < (kw + mw) * F; i += blockDim.x) zb[i] = 0u;
+    for (int i = threadIdx.x; i < 2 * F; i += blockDim.x) bad[i] = 0;
+    if (threadIdx.x < 4) flags[threadIdx.x] = -1;
+    if (threadIdx.x == 4) flags[4] = 0;
+    const int lane = threadIdx.x & 63;
+    const int wave = uniform(threadIdx.x >> 6);
+    const int j = lane / F, f = lane % F;
+    const int fr = tile * kTile + sub * F + f;  // this lane's frame
+    if (wave == 0 && j == 0) livel[f] = st.done[fr] == 0 ? 1 : 0;
+    __syncthreads();
+    if (!st.tile_active[tile]) return;
+
+    SubCtx<Q> c;
+    c.col_idx = col_idx;
+    c.row_ptr = row_ptr;
+    const size_t lo = (size_t)sub * F + f;
+    c.Eb = st.E + (size_t)tile * g.nnz * kTile + lo;
+    c.Lb = st.L + (size_t)tile * g.n * kTile + lo;
+    c.Cb = st.ch + (size_t)tile * g.n * kTile + lo;
+    c.Tb = st.T + (size_t)blockIdx.x * g.max_row_deg * F + f;
+    c.S = S + f;
+    c.dummy = (double *)(lds + ly.dummy) + f;
+    c.slot = (double *)(lds + ly.slot) + f;
+    c.ib = ib + f;
+    c.flag = flags;
+    c.tinyf = flags + 2;
+    c.tseq = flags + 4;
+    c.ttab = LdsTanh{mlds.tanh};
+    c.ltab = LdsLog{mlds.log};
+    c.ac = ac;
+    c.k = g.k;
+    c.wave = wave;
+    c.j = j;
+    c.f = f;
+    c.ntiny = 0;
+    const int m = g.m;
+    const int nthr = kSW * Q;       // (wavefront, lane group) pairs
+    const int me = wave * Q + j;    // this lane's pair
+
+    for (int it = 0; it < max_iter; ++it) {
+        c.first = it == 0;
+        c.live = livel[f] != 0;
+        c.ep0 = it * m;
+        double tA[K], tB[K];
+        bool yA = false, yB = false;
+        if (m > 0) yA = sub_p1(c, sub_chunk(row_ptr, 0, wave, Q), tA);
+        for (int r = 0; r <= m; r += 2) {
+            sub_body(c, r, m, tA, yA, tB, yB);
+            if (r + 1 <= m) sub_body(c, r + 1, m, tB, yB, tA, yA);
+        }
+        __syncthreads();  // every P3 done: S complete, identity bits set
+
+        // posteriors of the A columns (channel added after the sum), the
+        // normalized-LLR count against the previous posterior (:210-228),
+        // z^1 bits
+        int my_cnt = 0;
+        for (int col = me; col < g.k; col += nthr) {
+            double *sp = c.S + (size_t)col * F;
+            const double Sj = *sp;
+            *sp = 0.0;
+            const double chj = c.Cb[(size_t)col * kTile];
+            const double Lj = chj + Sj;
+            if (nllr) {
+                const double ap = c.first ? chj : ld_l2(c.Lb + (size_t)col * kTile);
+                my_cnt += (fabs(Lj) <= 7.0 && ap * Lj < 0.0) ? 1 : 0;
+            }
+            if (c.live) c.Lb[(size_t)col * kTile] = Lj;
+            if (!(Lj < 0.0)) atomicOr(zb + (col >> 5) * F + f, 1u << (col & 31));
+        }
+        if (nllr && my_cnt) atomicAdd(cntl + f, my_cnt);
+        __syncthreads();
+
+        // syndrome (:191-204): parity of row r = popcount(A_r & (z^1)_A) +
+        // (z^1)_{k+r}, A_r bit-packed
+        uint32_t acc = 0u;
+        for (int r = me; r < m; r += nthr) {
+            const uint32_t *ar = g.a_packed + (size_t)r * kw;
+            uint32_t par = ib[(r >> 5) * F + f] >> (r & 31);
+            for (int w = 0; w < kw; ++w) par += __builtin_popcount(ar[w] & zb[w * F + f]);
+            acc |= par & 1u;
+        }
+        if (acc) atomicOr((uint32_t *)bad + f, 1u);
+        __syncthreads();
+
+        if (wave == 0) {  // per-frame exits, as vn_kernel (static schedule)
+            bool still = false;
+            if (j == 0 && c.live) {
+                if (nllr) {
+                    const int cn = cntl[f];
+                    st.nllr_cnt[fr] = cn;
+                    if (st.nllr_hist)
+                        st.nllr_hist[(size_t)fr * st.hist_stride + it] = g.k > 0 ? (double)cn / g.k : 0.0;
+                }
+                if (bad[f] == 0) {  // syndrome zero: Result.OK at this iteration (:231-241)
+                    st.done[fr] = 1;
+                    st.conv[fr] = it;
+                    st.status[fr] = 0;
+                    st.iters[fr] = it + 1;
+                } else if (it == max_iter - 1) {  // Result.DATA_TRANSFER_NOT_OK (:244-253)
+                    st.done[fr] = 1;
+                    st.conv[fr] = -1;
+                    st.status[fr] = 1;
+                    st.iters[fr] = it + 1;
+                } else {
+                    still = true;
+                }
+            }
+            const unsigned long long any = __ballot(still);
+            if (j == 0) {
+                livel[f] = still ? 1 : 0;
+                bad[f] = 0;
+                cntl[f] = 0;
+            }
+            if (lane == 0) flags[5] = any != 0ull ? 1 : 0;
+        }
+        for (int i = threadIdx.x; i < (kw + mw) * F; i += blockDim.x) zb[i] = 0u;
+        __syncthreads();
+        if (!flags[5]) break;
+    }
+}
+
+template <int Q>
+size_t sub_lds_bytes_q(const DevGraph &g) {
+    constexpr int F = SubCfg<Q>::F, K = SubCfg<Q>::K;
+    if (!g.std_form || !g.a_packed || g.k <= 0 || g.max_row_deg > kSW * Q * K) return 0;
+    const size_t b = sub_layout(g.k, g.m, F).total;
+    return b <= kSubLdsMax ? b : 0;
+}
+
+}  // namespace
+
+// Frames per workgroup of the sub-tile decoder for this graph: 16, 8, or 0
+// (does not apply).
+int sub_frames(const DevGraph &g) {
+    if (sub_lds_bytes_q<4>(g)) return 16;
+    if (sub_lds_bytes_q<8>(g)) return 8;
+    return 0;
+}
+size_t sub_lds_bytes(const DevGraph &g) {
+    const int F = sub_frames(g);
+    return F == 16 ? sub_lds_bytes_q<4>(g) : F == 8 ? sub_lds_bytes_q<8>(g) : 0;
+}
+
+hipError_t launch_tile_sub(const DevGraph &g, const DevState &st, int max_iter, bool nllr, hipStream_t s) {
+    const int F = sub_frames(g);
+    const size_t lds = sub_lds_bytes(g);
+    if (!F || !lds) return hipErrorInvalidValue;
+    if (F == 16)
+        tile_sub_kernel<4><<<st.ntiles * 4, 64 * kSW, lds, s>>>(g, st, max_iter, nllr ? 1 : 0, g.col_idx, g.row_ptr,
+                                                                kAtanhCoef);
+    else
+        tile_sub_kernel<8><<<st.ntiles * 8, 64 * kSW, lds, s>>>(g, st, max_iter, nllr ? 1 : 0, g.col_idx, g.row_ptr,
+                                                                kAtanhCoef);
+    return hipGetLastError();
+}
+
+}  // namespace ldpc

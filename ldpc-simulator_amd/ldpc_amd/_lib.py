@@ -25,7 +25,7 @@ EXPORTED = (
     "ldpc_last_error", "ldpc_abi_version", "ldpc_device_count",
     "ldpc_hstd_build", "ldpc_hstd_get", "ldpc_hstd_free",
     "ldpc_graph_create", "ldpc_graph_destroy", "ldpc_graph_info", "ldpc_cn_kernel_name",
-    "ldpc_phys_kernel_name", "ldpc_tile_lds_bytes",
+    "ldpc_phys_kernel_name", "ldpc_tile_lds_bytes", "ldpc_tile_kernel_name",
     "ldpc_decoder_bytes", "ldpc_decoder_create", "ldpc_decoder_destroy", "ldpc_decoder_capacity",
     "ldpc_decode_f64", "ldpc_generate_frames", "ldpc_mc_run",
     "ldpc_profile_enable", "ldpc_profile_read",
@@ -64,6 +64,7 @@ def _declare(lib):
         "ldpc_cn_kernel_name": (ctypes.c_char_p, [c_vp]),
         "ldpc_phys_kernel_name": (ctypes.c_char_p, [c_vp, ctypes.c_uint32]),
         "ldpc_tile_lds_bytes": (ctypes.c_int64, [c_vp]),
+        "ldpc_tile_kernel_name": (ctypes.c_char_p, [c_vp]),
         "ldpc_decoder_bytes": (c_i64, [c_vp, c_i32]),
         "ldpc_decoder_create": (ctypes.c_int, [c_vp, c_i32, P(c_vp)]),
         "ldpc_decoder_destroy": (ctypes.c_int, [c_vp]),

@@ -88,3 +88,44 @@ def test_tile_mc_counters_equal_split(gpu_available):
     a = dec.mc_run(20260213, sig, 2048, 0, 20, nllr=True, static=True)
     b = dec.mc_run(20260213, sig, 2048, 0, 20, nllr=True, static=True, split=True)
     np.testing.assert_array_equal(a, b)
+
+
+# --- sub-tile decoder (tile_sub.hip): the WiMAX 2304 codes, 16 or 8 frames per
+# workgroup, lane groups sharing one wavefront's chunk of a check row
+
+
+def test_sub_tile_is_the_one_launched(gpu_available):
+    from ldpc_amd import _lib
+    for code in ("wimax_2304_0.5", "wimax_2304_0.75A"):
+        dec = _decoder(code, 64)
+        assert _lib.lib().ldpc_tile_kernel_name(dec.graph.handle) == b"tile_sub_kernel"
+        llr = _random_llr(hstd_for(code), 64, 1.0, seed=2)
+        dec.profile(True)
+        dec.decode(llr, 2)
+        p = dec.profile_read()
+        dec.profile(False)
+        assert p["tile"][1] == 1 and p["cn"][1] == 0 and p["vn"][1] == 0, p
+
+
+@pytest.mark.parametrize("code,snr,T,B", [("wimax_2304_0.5", 0.0, 4, 70), ("wimax_2304_0.5", 3.0, 25, 40),
+                                          ("wimax_2304_0.75A", 2.0, 5, 64), ("wimax_2304_0.75B", 4.0, 8, 24)])
+def test_sub_tile_bit_identical_to_split(gpu_available, code, snr, T, B):
+    llr = _random_llr(hstd_for(code), B, snr, seed=int(100 * snr) + 2000 + T)
+    dec = _decoder(code, B)
+    a = dec.decode(llr, T, nllr=True, post=True, hist=True, msgs=True)
+    b = dec.decode(llr, T, nllr=True, post=True, hist=True, msgs=True, split=True)
+    _assert_identical(a, b)
+
+
+def test_sub_tile_rare_rows_identical(gpu_available):
+    code = "wimax_2304_0.5"
+    H = hstd_for(code)
+    llr = _random_llr(H, 80, 1.0, seed=19)
+    llr[0, :] = 0.0
+    llr[5, ::7] = 0.0
+    llr[17, :] = 1e-13
+    llr[66, ::3] = 0.0  # another 64-frame tile, another sub-tile
+    dec = _decoder(code, 80)
+    for T in (1, 3):
+        _assert_identical(dec.decode(llr, T, nllr=True, post=True, msgs=True),
+                          dec.decode(llr, T, nllr=True, post=True, msgs=True, split=True))
