@@ -274,7 +274,7 @@ def main():
 
     tile_ms, tile_launches = prof.get("tile", (0.0, 0))
     if tile_launches:  # tile-resident decoder: one launch decodes a chunk through all its iterations
-        cn_name = "tile_kernel"
+        cn_name = _lib.lib().ldpc_tile_kernel_name(graph.handle).decode() or "tile_kernel"
         decode_ms = tile_ms
         decode_gbs = dec_bytes / (decode_ms / 1e3) / 1e9 if decode_ms else 0.0
     out = {
@@ -321,7 +321,7 @@ def main():
             "bound": "hbm", "achieved": decode_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": decode_gbs / HBM_PEAK_GBS, "traffic": committed_traffic(nnz, chunk, "tile")[0],
             "traffic_source": committed_traffic(nnz, chunk, "tile")[1],
-            "kernel": "tile_kernel", "launches": tile_launches, "avg_launch_ms": tile_ms / tile_launches,
+            "kernel": cn_name, "launches": tile_launches, "avg_launch_ms": tile_ms / tile_launches,
             "bytes_per_launch": dec_bytes / tile_launches,
             "bytes_model": "per frame 8 n (channel LLRs) + 16 B x H_std edges x iterations executed "
                            "(E_old read + E_new write) + ceil(n/8) + 8 (SURVEY 8d); CN and VN fused",

@@ -25,6 +25,11 @@
 //             P1(r+1)  L[col], E_old, t = tanh((L - E_old)/2) (:138-146,
 //                      :260-268).
 //
+// Opt-in (LDPC_TILE_SUB=1): bit-identical to the split path, but slower on
+// every 2304 code measured -- the in-wavefront hand-over costs
+// Q rounds of products and two ds_bpermute per hop on the row's critical path,
+// and F = 8 reads half cache lines.
+//
 // Per edge and iteration the HBM traffic is the algorithmic 16 B (E_old read,
 // E_new write) plus the L[col] gather (8 B, L2/MALL): the split CN/VN
 // launches this replaces move 24 + 8 B plus the gathers.  The identity column

@@ -91,10 +91,22 @@ def test_tile_mc_counters_equal_split(gpu_available):
 
 
 # --- sub-tile decoder (tile_sub.hip): the WiMAX 2304 codes, 16 or 8 frames per
-# workgroup, lane groups sharing one wavefront's chunk of a check row
+# workgroup, lane groups sharing one wavefront's chunk of a check row; opt-in
+# (LDPC_TILE_SUB=1, read by the library at every decode)
 
 
-def test_sub_tile_is_the_one_launched(gpu_available):
+@pytest.fixture
+def sub_tile(monkeypatch):
+    monkeypatch.setenv("LDPC_TILE_SUB", "1")
+
+
+def test_sub_tile_is_opt_in(gpu_available):
+    from ldpc_amd import _lib
+    dec = _decoder("wimax_2304_0.5", 64)
+    assert _lib.lib().ldpc_tile_kernel_name(dec.graph.handle) == b""
+
+
+def test_sub_tile_is_the_one_launched(gpu_available, sub_tile):
     from ldpc_amd import _lib
     for code in ("wimax_2304_0.5", "wimax_2304_0.75A"):
         dec = _decoder(code, 64)
@@ -109,7 +121,7 @@ def test_sub_tile_is_the_one_launched(gpu_available):
 
 @pytest.mark.parametrize("code,snr,T,B", [("wimax_2304_0.5", 0.0, 4, 70), ("wimax_2304_0.5", 3.0, 25, 40),
                                           ("wimax_2304_0.75A", 2.0, 5, 64), ("wimax_2304_0.75B", 4.0, 8, 24)])
-def test_sub_tile_bit_identical_to_split(gpu_available, code, snr, T, B):
+def test_sub_tile_bit_identical_to_split(gpu_available, sub_tile, code, snr, T, B):
     llr = _random_llr(hstd_for(code), B, snr, seed=int(100 * snr) + 2000 + T)
     dec = _decoder(code, B)
     a = dec.decode(llr, T, nllr=True, post=True, hist=True, msgs=True)
@@ -117,7 +129,7 @@ def test_sub_tile_bit_identical_to_split(gpu_available, code, snr, T, B):
     _assert_identical(a, b)
 
 
-def test_sub_tile_rare_rows_identical(gpu_available):
+def test_sub_tile_rare_rows_identical(gpu_available, sub_tile):
     code = "wimax_2304_0.5"
     H = hstd_for(code)
     llr = _random_llr(H, 80, 1.0, seed=19)
