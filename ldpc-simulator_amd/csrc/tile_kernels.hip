@@ -134,6 +134,11 @@ __host__ __device__ inline TileLayout tile_layout(int k, int m) {
 #define LDPC_TILE_SMALLQ 0
 #endif
 //   LDPC_TILE_GROUP     edges per straight-line group in the P1 / P3 math
+//   LDPC_TILE_STORE1    1: P3 stores the chunk's E_new in one live-masked
+//                       block (one exec-mask switch per chunk, not per edge)
+#ifndef LDPC_TILE_STORE1
+#define LDPC_TILE_STORE1 1
+#endif
 #ifndef LDPC_TILE_GROUP
 #define LDPC_TILE_GROUP 1
 #endif
@@ -394,13 +399,19 @@ __device__ __forceinline__ void tile_p3(TileCtx &c, int r, double (&t)[kTK], con
             }
         }
     }
+    constexpr bool store1 = LDPC_TILE_STORE1 && !LDPC_TILE_P3FUSED && !LDPC_TILE_PREFETCH;
+    if (store1 && c.live) {  // the chunk's E_new stores under ONE exec mask
+#pragma unroll
+        for (int i = 0; i < kTK; ++i)
+            if (i < rc.cnt) *at(c.Eb, rc.c0 + i, c.lane) = t[i];
+    }
 #pragma unroll
     for (int i = 0; i < kTK; ++i) {
         if (i < rc.cnt) {
             if (fused) t[i] = 2.0 * atanh_f(clip_cl(P / t[i]), c.ltab, c.ac);  // :159-168
             const int e = rc.c0 + i;
             const int col = c.col_idx[e];
-            if (c.live) *at(c.Eb, e, c.lane) = t[i];
+            if (!store1 && c.live) *at(c.Eb, e, c.lane) = t[i];
             if (col < c.k) {  // S_col += E (rows ascending)
                 double *sp = c.S + col * kTile + c.lane;
                 *sp = *sp + t[i];
