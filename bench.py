@@ -74,7 +74,10 @@ def dist_setup(args):
         import torch.distributed as dist
         device = local % max(1, torch.cuda.device_count())
         torch.cuda.set_device(device)
-        dist.init_process_group(args.dist_backend)  # "nccl" is RCCL on ROCm
+        if args.dist_backend == "nccl":  # RCCL on ROCm; bind the rank's GPU explicitly
+            dist.init_process_group("nccl", device_id=torch.device(f"cuda:{device}"))
+        else:
+            dist.init_process_group(args.dist_backend)
     return world, rank, device, dist
 
 
@@ -326,6 +329,11 @@ def main():
             "bytes_model": "per frame 8 n (channel LLRs) + 16 B x H_std edges x iterations executed "
                            "(E_old read + E_new write) + ceil(n/8) + 8 (SURVEY 8d); CN and VN fused",
         }
+        # the north_star's "HBM-read roofline": the read part alone, 8 n + 8 B x edges x iterations
+        read_bytes = frames_local * 8 * n + 8.0 * nnz * local_iters
+        read_gbs = read_bytes / (decode_ms / 1e3) / 1e9 if decode_ms else 0.0
+        out["roofline"]["read_achieved"] = read_gbs
+        out["roofline"]["read_frac"] = read_gbs / HBM_PEAK_GBS
     if pgraph is not None:  # physical mode (not the reference's arithmetic: §8 f4)
         pnnz = int(pgraph.nnz)
         pms, pl = prof["phys"]
