@@ -1006,6 +1006,11 @@ int ldpc_phys_mc_run(ldpc_decoder *d, const ldpc_graph *gp, uint64_t seed, int32
 }
 
 // -------------------------------------------------------------- profiling
+int ldpc_diag_tile_trace(uint64_t *out, int64_t n) {
+    if (!out || n <= 0) return ldpc_fail(LDPC_EINVAL, "ldpc_diag_tile_trace: no buffer");
+    return ldpc::tile_trace_read((unsigned long long *)out, (size_t)n);
+}
+
 int ldpc_profile_enable(ldpc_decoder *d, int enable) {
     if (!d) return ldpc_fail(LDPC_EINVAL, "ldpc_profile_enable: NULL decoder");
     d->prof = enable != 0;

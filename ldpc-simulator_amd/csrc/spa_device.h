@@ -80,6 +80,7 @@ size_t tile_lds_bytes(const DevGraph &g);
 const char *tile_kernel_name(const DevGraph &g);  // "tile_kernel", "tile_sub_kernel" or ""
 bool use_tile(const DevGraph &g);
 hipError_t launch_tile(const DevGraph &g, const DevState &st, int max_iter, bool nllr, hipStream_t s);
+int tile_trace_read(unsigned long long *out, size_t n);  // LDPC_TILE_TRACE builds
 int sub_frames(const DevGraph &g);
 size_t sub_lds_bytes(const DevGraph &g);
 hipError_t launch_tile_sub(const DevGraph &g, const DevState &st, int max_iter, bool nllr, hipStream_t s);

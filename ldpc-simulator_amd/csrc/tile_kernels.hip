@@ -149,6 +149,23 @@ constexpr int kTG = LDPC_TILE_GROUP;
 #define LDPC_TILE_CONST_COEF 0
 #endif
 
+// LDPC_TILE_TRACE (diagnostic build): s_memtime stamps of every wavefront of
+// workgroup 0 at the phase boundaries of rows 0..kTrRows-1 of pass 2, read
+// back with ldpc_diag_tile_trace (ldpc_api.cpp); tools/tile_trace.py.
+constexpr int kTrRows = 64, kTrEv = 8;
+#ifdef LDPC_TILE_TRACE
+__device__ unsigned long long g_tile_trace[kTW][kTrRows][kTrEv];
+#define TSTAMP(c, r, ev)                                                                              \
+    do {                                                                                              \
+        if (blockIdx.x == 0 && (c).ep0 == 2 * (c).m_ && (r) < kTrRows && (c).lane == 0)               \
+            g_tile_trace[(c).wave][(r)][(ev)] = __builtin_amdgcn_s_memtime();                         \
+    } while (0)
+#else
+#define TSTAMP(c, r, ev) \
+    do {                 \
+    } while (0)
+#endif
+
 // element (item, lane) of a tile array
 template <class T>
 __device__ __forceinline__ T *at(T *base, int item, uint32_t lane) {
@@ -190,6 +207,7 @@ struct TileCtx {
     int k, wave;
     uint32_t lane;
     int ep0;  // epoch of row 0 in this pass (flags are tagged (epoch, stage))
+    int m_;   // rows (trace builds)
     bool first, live;
     int ntiny;
 };
@@ -271,6 +289,31 @@ __device__ __forceinline__ bool tile_p1_math(const TileCtx &c, const RowChunk &r
     return __ballot(tiny) != 0ull;
 }
 
+// P * t[0] * t[1] * ... * t[cnt-1], left to right, as exactly cnt dependent
+// multiplies: one uniform branch on cnt selects a straight-line sequence (a
+// guarded loop was if-converted into mul + 2 v_cndmask per slot for all kTK
+// slots -- 3x the dependent chain on the row's critical path).
+template <int N>
+__device__ __forceinline__ double mul_n(double P, const double (&t)[kTK]) {
+#pragma unroll
+    for (int i = 0; i < N; ++i) P = P * t[i];
+    return P;
+}
+template <int N>
+struct ChainMul {
+    static __device__ __forceinline__ double run(double P, const double (&t)[kTK], int cnt) {
+        if (cnt == N) return mul_n<N>(P, t);
+        return ChainMul<N - 1>::run(P, t, cnt);
+    }
+};
+template <>
+struct ChainMul<0> {
+    static __device__ __forceinline__ double run(double P, const double (&)[kTK], int) { return P; }
+};
+#ifndef LDPC_TILE_CHAINSW
+#define LDPC_TILE_CHAINSW 1
+#endif
+
 // hop: this wavefront's segment of row r's left-to-right product.
 __device__ __forceinline__ void tile_hop(const TileCtx &c, int r, const double (&t)[kTK], bool tiny) {
     const RowChunk rc = chunk_of(c.row_ptr, r, c.wave);
@@ -281,22 +324,33 @@ __device__ __forceinline__ void tile_hop(const TileCtx &c, int r, const double (
     double P;
     if (LDPC_TILE_PRIO) __builtin_amdgcn_s_setprio(2);
     if (c.wave == 0) {
-        P = t[0];  // wavefront 0 always holds the row's first edge
+        if (LDPC_TILE_CHAINSW) {
+            P = ChainMul<kTK>::run(1.0, t, rc.cnt);  // 1.0 * t0 == t0 exactly
+        } else {
+            P = t[0];  // wavefront 0 always holds the row's first edge
 #pragma unroll
-        for (int i = 1; i < kTK; ++i)
-            if (i < rc.cnt) P = P * t[i];
+            for (int i = 1; i < kTK; ++i)
+                if (i < rc.cnt) P = P * t[i];
+        }
         if (c.lane == 0) lds_st(c.tinyf + s, tiny ? 1 : 0);
     } else {
+        TSTAMP(c, r, 3);
         wait_flag(c.flag + s, ep + c.wave);
+        TSTAMP(c, r, 4);
         P = *sl;
+        if (LDPC_TILE_CHAINSW) {
+            P = ChainMul<kTK>::run(P, t, rc.cnt);
+        } else {
 #pragma unroll
-        for (int i = 0; i < kTK; ++i)
-            if (i < rc.cnt) P = P * t[i];
+            for (int i = 0; i < kTK; ++i)
+                if (i < rc.cnt) P = P * t[i];
+        }
         if (tiny && c.lane == 0) lds_st(c.tinyf + s, 1);
     }
     *sl = P;
     lds_release();
     if (c.lane == 0) lds_st(c.flag + s, ep + c.wave + 1);
+    TSTAMP(c, r, 5);
     if (LDPC_TILE_PRIO) __builtin_amdgcn_s_setprio(0);
 }
 
@@ -327,7 +381,9 @@ __device__ __forceinline__ void tile_p3(TileCtx &c, int r, double (&t)[kTK], con
     }
     const int s = r & (kTR - 1);
     const int ep = ((c.ep0 + r) & 0x3ffffff) * 32;
+    TSTAMP(c, r, 0);
     wait_flag(c.flag + s, ep + kTW);
+    TSTAMP(c, r, 1);
     const double P = c.slot[s * kTile + c.lane];
     const bool tiny_row = uniform(lds_ld(c.tinyf + s)) != 0;
     const bool fused = LDPC_TILE_P3FUSED && !tiny_row;
@@ -442,6 +498,7 @@ __device__ __forceinline__ void tile_body(TileCtx &c, int r, int m, double (&tcu
         if (r >= 1) tile_p3(c, r - 1, toth, rc1, eo);
     } else {
         if (r >= 1) tile_p3(c, r - 1, toth, rc1, eo);
+        if (r >= 1) TSTAMP(c, r - 1, 2);
         if (r < m) tile_hop(c, r, tcur, ycur);
     }
     if (r + 1 < m) {
@@ -449,6 +506,7 @@ __device__ __forceinline__ void tile_body(TileCtx &c, int r, int m, double (&tcu
             yoth = tile_p1_math(c, rc1, toth, eo);
         } else {
             yoth = tile_p1(c, rc1, toth);
+            TSTAMP(c, r + 1, 6);
         }
     }
 }
@@ -570,6 +628,7 @@ __global__ __launch_bounds__(64 * kTW, 1) void tile_kernel(DevGraph g, DevState 
     c.lane = lane;
     c.wave = wave;
     c.ntiny = 0;
+    c.m_ = g.m;
     const int m = g.m;
 
     for (int it = 0; it < max_iter; ++it) {
@@ -611,6 +670,19 @@ __global__ __launch_bounds__(64 * kTW, 1) void tile_kernel(DevGraph g, DevState 
 
 
 }  // namespace
+
+// diagnostic: copy the trace stamps (LDPC_TILE_TRACE builds; else returns -1)
+int tile_trace_read(unsigned long long *out, size_t n) {
+#ifdef LDPC_TILE_TRACE
+    const size_t b = sizeof(unsigned long long) * (size_t)kTW * kTrRows * kTrEv;
+    if (n * sizeof(unsigned long long) < b) return -1;
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_tile_trace), b) == hipSuccess ? (int)(b / 8) : -1;
+#else
+    (void)out;
+    (void)n;
+    return -1;
+#endif
+}
 
 size_t tile64_lds_bytes(const DevGraph &g) {
     if (!g.std_form || !g.a_packed || g.k <= 0 || g.k > 32 * kTKW || g.max_row_deg > kTW * kTK) return 0;
