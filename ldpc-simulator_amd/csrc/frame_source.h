@@ -53,4 +53,62 @@ __device__ __forceinline__ double channel_llr(uint32_t bit, double g, double s2)
     return (2.0 * y) / s2;
 }
 
+
+__device__ __forceinline__ unsigned long long wave_sum(unsigned long long v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    return v;
+}
+
+// ------------------------------------------------ per-lane frame generation
+// (streaming refill; whole chunks use frame_kernels.hip).  u bits live in LDS
+// ([kw][64], each lane reads only its own column, so no barrier is needed).
+// Frame F of SNR point `snr_point` into lane `lane` of `tile`: info bits (ubits
+// and the lane's LDS column `ul`), channel LLRs ch[tile][j][lane].  With
+// `set_L`, also L = ch (a streaming refill: the next CN then forms M = L - 0).
+__device__ inline void gen_lane(const DevGraph &g, const DevState &st, int tile, int lane, int64_t F, uint64_t seed,
+                         int snr_point, double sigma, const uint32_t *__restrict__ apack, uint32_t *ul, bool valid,
+                         bool set_L) {
+    const int kw = (g.k + 31) >> 5;
+    // info bits: data_buffer.py:23 / generator.py:7-9 (random.randint(0,1) per bit)
+    for (int blk = 0; blk * 4 < kw; ++blk) {
+        uint32_t c[4];
+        info_block(seed, F, snr_point, blk, c);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int w = blk * 4 + q;
+            if (w >= kw) break;
+            uint32_t v = c[q];
+            if (w == kw - 1 && (g.k & 31)) v &= (1u << (g.k & 31)) - 1u;
+            ul[w * kTile + lane] = v;
+            st.ubits[((size_t)tile * kw + w) * kTile + lane] = v;
+        }
+    }
+    // codeword [u, A.u mod 2] + BPSK + AWGN (channel.py:49,68-80)
+    const double s2 = sigma * sigma;
+    double *Ct = st.ch + (size_t)tile * g.n * kTile + lane;
+    double *Lt = st.L + (size_t)tile * g.n * kTile + lane;
+    for (int jb = 0; jb < g.n; jb += 2) {
+        double gz[2];
+        noise_pair(seed, F, snr_point, jb >> 1, gz);
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+            const int j = jb + q;
+            if (j >= g.n) break;
+            uint32_t bit;
+            if (j < g.k) {
+                bit = (ul[(j >> 5) * kTile + lane] >> (j & 31)) & 1u;
+            } else {  // parity bit of row j-k = parity(A_row & u), A bit-packed (uniform loads)
+                const uint32_t *ar = apack + (size_t)(j - g.k) * kw;
+                uint32_t acc = 0u;
+                for (int w = 0; w < kw; ++w) acc ^= ar[w] & ul[w * kTile + lane];
+                bit = (uint32_t)__popc(acc) & 1u;
+            }
+            const double llr = valid ? channel_llr(bit, gz[q], s2) : 0.0;
+            Ct[j * kTile] = llr;
+            if (set_L) Lt[j * kTile] = llr;
+        }
+    }
+}
+
 }  // namespace ldpc

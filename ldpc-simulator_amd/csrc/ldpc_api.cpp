@@ -689,7 +689,7 @@ namespace {
 // chunk; only the last frames of the point form a tail.  Frames, and the
 // counters summed over them, are exactly the static schedule's.
 int mc_stream_point(ldpc_decoder *d, uint64_t seed, int p, double sigma, int64_t total, int64_t frame0, int max_iter,
-                    bool nllr, hipStream_t s) {
+                    bool nllr, bool split, hipStream_t s) {
     if (total == 0) return LDPC_OK;
     const DevGraph &G = d->g->dg;
     const int ntiles = (int)std::min<int64_t>(d->cap_tiles, (total + kTile - 1) / kTile);
@@ -697,6 +697,14 @@ int mc_stream_point(ldpc_decoder *d, uint64_t seed, int p, double sigma, int64_t
     const DevState st = d->st;
     unsigned long long *ctr = d->counters + (size_t)p * LDPC_MC_NCOUNT;
     unsigned long long *next = d->counters + d->counters_cap;
+    if (!split && ldpc::use_tile_stream(G) && st.ntiles <= st.nslots) {
+        // one launch: every workgroup's lanes pull frames until the supply is out
+        HIP_TRY(hipMemsetAsync(next, 0, sizeof(unsigned long long), s));
+        HIP_TRY(timed(d, LDPC_K_TILE, s, [&] {
+            return ldpc::launch_tile_stream(G, st, max_iter, nllr, seed, p, sigma, frame0, total, next, ctr, s);
+        }));
+        return LDPC_OK;
+    }
     HIP_TRY(ldpc::launch_stream_init(G, st, s));
     HIP_TRY(hipMemsetAsync(next, 0, sizeof(unsigned long long), s));
     auto refill = [&] {
@@ -757,7 +765,9 @@ int ldpc_mc_run(ldpc_decoder *d, uint64_t seed, int32_t n_points, const double *
     const int64_t cap = (int64_t)d->cap_tiles * kTile;
     if (!(flags & LDPC_F_STATIC)) {
         for (int p = 0; p < n_points; ++p)
-            if (int rc = mc_stream_point(d, seed, p, sigmas[p], frames_per_point, frame0, max_iter, nllr, s)) return rc;
+            if (int rc = mc_stream_point(d, seed, p, sigmas[p], frames_per_point, frame0, max_iter, nllr,
+                                         flags & LDPC_F_SPLIT, s))
+                return rc;
     } else {
     if (int rc = ensure_pbits(d, G)) return rc;
     for (int p = 0; p < n_points; ++p) {

@@ -81,6 +81,12 @@ const char *tile_kernel_name(const DevGraph &g);  // "tile_kernel", "tile_sub_ke
 bool use_tile(const DevGraph &g);
 hipError_t launch_tile(const DevGraph &g, const DevState &st, int max_iter, bool nllr, hipStream_t s);
 int tile_trace_read(unsigned long long *out, size_t n);  // LDPC_TILE_TRACE builds
+// Streaming Monte-Carlo through the tile-resident decoder (one launch per SNR
+// point; LDPC_TILE_STREAM=0 keeps the split CN/VN/refill loop).
+bool use_tile_stream(const DevGraph &g);
+hipError_t launch_tile_stream(const DevGraph &g, const DevState &st, int max_iter, bool nllr, uint64_t seed,
+                              int snr_point, double sigma, int64_t frame0, int64_t total, unsigned long long *next,
+                              unsigned long long *ctr, hipStream_t s);
 int sub_frames(const DevGraph &g);
 size_t sub_lds_bytes(const DevGraph &g);
 hipError_t launch_tile_sub(const DevGraph &g, const DevState &st, int max_iter, bool nllr, hipStream_t s);

@@ -57,6 +57,7 @@
 #include "tile_common.h"
 #include "spa_device.h"
 #include "spa_math.h"
+#include "frame_source.h"
 
 namespace ldpc {
 namespace {
@@ -209,6 +210,7 @@ struct TileCtx {
     int ep0;  // epoch of row 0 in this pass (flags are tagged (epoch, stage))
     int m_;   // rows (trace builds)
     bool first, live;
+    bool fresh;  // streaming: this lane's frame is on its first pass (M = L - 0)
     int ntiny;
 };
 
@@ -230,7 +232,7 @@ __device__ __forceinline__ double tile_load_e(const TileCtx &c, const RowChunk &
     return c.first ? 0.0 : *at(c.Eb, rc.c0 + min(i, rc.cnt - 1), c.lane);
 }
 __device__ __forceinline__ bool tile_t(const TileCtx &c, double &t, double eo) {
-    const double M = c.first ? t : t - eo;  // :85-90 / :260-268
+    const double M = c.first ? t : t - (c.fresh ? 0.0 : eo);  // :85-90 / :260-268
 #ifdef LDPC_TILE_DIAG_NOTANH  // diagnostic (WRONG results): tanh as one fma
     t = __builtin_fma(M, 0.125, 0.25);
     return false;
@@ -629,6 +631,7 @@ __global__ __launch_bounds__(64 * kTW, 1) void tile_kernel(DevGraph g, DevState 
     c.wave = wave;
     c.ntiny = 0;
     c.m_ = g.m;
+    c.fresh = false;
     const int m = g.m;
 
     for (int it = 0; it < max_iter; ++it) {
@@ -668,6 +671,208 @@ __global__ __launch_bounds__(64 * kTW, 1) void tile_kernel(DevGraph g, DevState 
     }
 }
 
+
+
+// ---------------------------------------------------------------------------
+// Streaming tile decoder (Monte-Carlo, tile_stream_kernel).  With the static
+// schedule a tile runs until its slowest frame stops: at 3 dB on wimax_576_0.5
+// (2.9 iterations on average, FER 1.9 %) most tiles hold a 50-iteration frame,
+// so the step costs nearly 50 passes.  Here every lane is a slot at its own
+// iteration: after each pass a lane whose frame stopped adds that frame's
+// counters (count_kernel's definitions, main.py:130-138) and takes the next
+// frame index from one device counter; the frame is generated in place
+// (gen_lane: ch and L = ch, so the next pass forms M = L - 0, its iteration
+// 0).  Every frame is decoded exactly as in the static schedule (the lane's
+// state depends on its own frame only), so the counters are identical.  The
+// workgroup exits once the supply is exhausted and its lanes have drained.
+// wave 0 of the streaming kernel: lanes with `want` take the next frame
+// indices (one wave-aggregated atomicAdd) and generate them (inlined: as a
+// real call the register saves around it cost 10x).
+__device__ __forceinline__ void tile_refill(const DevGraph &g, const DevState &st, int tile, int lane, bool want,
+                                         uint64_t seed, int snr_point, double sigma, int64_t frame0, int64_t total,
+                                         unsigned long long *next, uint32_t *ul, int *livel, int *freshl, int *itl) {
+    const unsigned long long w = __ballot(want);
+    const int first = __ffsll((long long)w) - 1;
+    unsigned long long base = 0ull;
+    if (lane == first) base = atomicAdd(next, (unsigned long long)__popcll(w));
+    base = __shfl(base, first);
+    const unsigned long long below = lane ? (w & (~0ull >> (64 - lane))) : 0ull;
+    const int64_t idx = (int64_t)(base + (unsigned long long)__popcll(below));
+    const bool have = want && idx < total;
+    if (have) gen_lane(g, st, tile, lane, frame0 + idx, seed, snr_point, sigma, g.a_packed, ul, true, true);
+    if (want) {
+        livel[lane] = have ? 1 : 0;
+        freshl[lane] = have ? 1 : 0;
+        itl[lane] = 0;
+    }
+}
+
+__global__ __launch_bounds__(64 * kTW, 1) void tile_stream_kernel(DevGraph g, DevState st, int max_iter, int nllr,
+                                                                  const int *__restrict__ col_idx,
+                                                                  const int *__restrict__ row_ptr, AtanhCoef ac,
+                                                                  uint64_t seed, int snr_point, double sigma,
+                                                                  int64_t frame0, int64_t total,
+                                                                  unsigned long long *next,
+                                                                  unsigned long long *ctr) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+    const TileLayout ly = tile_layout(g.k, g.m);
+    double *S = (double *)(lds + ly.S);
+    MathLds &mlds = *(MathLds *)(lds + ly.math);
+    uint32_t *zb = (uint32_t *)(lds + ly.zb);
+    uint32_t *ib = (uint32_t *)(lds + ly.ib);
+    int *bad = (int *)(lds + ly.lane_i);
+    int *cntl = bad + kTile;
+    int *livel = cntl + kTile;
+    int *flags = (int *)(lds + ly.flags);
+    __shared__ int itl[kTile], freshl[kTile];
+    const int kw = (g.k + 31) >> 5, mw = (g.m + 31) >> 5;
+    const int tile = blockIdx.x;
+    if (tile >= st.ntiles) return;  // block-uniform
+
+    fill_math_lds(mlds);
+    for (int i = threadIdx.x; i < g.k * kTile; i += blockDim.x) S[i] = 0.0;
+    for (int i = threadIdx.x; i < (kw + mw) * kTile; i += blockDim.x) zb[i] = 0u;
+    for (int i = threadIdx.x; i < 2 * kTile; i += blockDim.x) bad[i] = 0;
+    if (threadIdx.x < 2 * kTR) flags[threadIdx.x] = -1;
+    if (threadIdx.x == 2 * kTR) flags[2 * kTR] = 0;
+    if (threadIdx.x >= 2 * kTR + 2 && threadIdx.x < 2 * kTR + 6) flags[threadIdx.x] = 0;
+    const int lane = threadIdx.x & 63;
+    const int wave = uniform(threadIdx.x >> 6);
+    bool want = true;  // wave 0: this lane asks for a frame
+    if (wave == 0) {
+        livel[lane] = 0;
+        itl[lane] = 0;
+        freshl[lane] = 0;
+    }
+
+    TileCtx c;
+    c.col_idx = col_idx;
+    c.row_ptr = row_ptr;
+    c.Eb = st.E + (size_t)tile * g.nnz * kTile;
+    c.Lb = st.L + (size_t)tile * g.n * kTile;
+    c.Cb = st.ch + (size_t)tile * g.n * kTile;
+    c.Tb = st.T + (size_t)blockIdx.x * g.max_row_deg * kTile;
+    c.S = S;
+    c.slot = (double *)(lds + ly.slot);
+    c.ib = ib;
+    c.flag = flags;
+    c.tinyf = flags + kTR;
+    c.tseq = flags + 2 * kTR;
+    c.p3n = flags + 2 * kTR + 2;
+    c.ttab = LdsTanh{mlds.tanh};
+    c.ltab = LdsLog{mlds.log};
+    c.ac = ac;
+    c.k = g.k;
+    c.lane = lane;
+    c.wave = wave;
+    c.ntiny = 0;
+    c.m_ = g.m;
+    c.first = false;
+    const int m = g.m;
+    const uint32_t *Ut = st.ubits + (size_t)tile * kw * kTile + lane;
+
+    for (int pass = 0;; ++pass) {
+        // refill: lanes without a frame take the next indices and generate
+        // them (wave 0, one frame per lane; u bits staged in zb)
+        if (wave == 0) {
+            if (__ballot(want) != 0ull)
+                tile_refill(g, st, tile, lane, want, seed, snr_point, sigma, frame0, total, next, zb, livel, freshl,
+                            itl);
+            want = false;
+            const unsigned long long any = __ballot(livel[lane] != 0);
+            if (lane == 0) flags[2 * kTR + 1] = any != 0ull ? 1 : 0;
+        }
+        __syncthreads();  // the generator staged u bits in zb: clear only after it
+        for (int i = threadIdx.x; i < kw * kTile; i += blockDim.x) zb[i] = 0u;
+        __syncthreads();
+        if (!flags[2 * kTR + 1]) break;  // supply exhausted, every lane drained
+
+        c.live = livel[lane] != 0;
+        c.fresh = freshl[lane] != 0;
+        c.ep0 = pass * m;
+        double tA[kTK], tB[kTK], eo[kTK];
+        bool yA = false, yB = false;
+        if (m > 0) yA = tile_p1(c, chunk_of(row_ptr, 0, wave), tA);
+        for (int r = 0; r <= m; r += 2) {
+            tile_body(c, r, m, tA, yA, tB, yB, eo);
+            if (r + 1 <= m) tile_body(c, r + 1, m, tB, yB, tA, yA, eo);
+        }
+        __syncthreads();
+
+        int my_cnt = 0;
+        for (int j = wave; j < g.k; j += kTW) {
+            double *sp = S + j * kTile + lane;
+            const double Sj = *sp;
+            *sp = 0.0;
+            const double chj = *at(c.Cb, j, lane);
+            const double Lj = chj + Sj;  // channel added after the sum (:173,185)
+            if (nllr) {
+                const double ap = ld_l2(at(c.Lb, j, lane));  // previous L (= ch on a frame's first pass)
+                my_cnt += (fabs(Lj) <= 7.0 && ap * Lj < 0.0) ? 1 : 0;
+            }
+            if (c.live) *at(c.Lb, j, lane) = Lj;
+            if (!(Lj < 0.0)) atomicOr(zb + (j >> 5) * kTile + lane, 1u << (j & 31));
+        }
+        if (nllr && my_cnt) atomicAdd(cntl + lane, my_cnt);
+        __syncthreads();
+
+        // syndrome (:191-204), as tile_pass_end
+        uint32_t acc = 0u;
+        {
+            uint32_t zr[kTKW];
+#pragma unroll
+            for (int w = 0; w < kTKW; ++w) zr[w] = w < kw ? zb[w * kTile + lane] : 0u;
+            for (int r = wave; r < m; r += kTW) {
+                const uint32_t *ar = g.a_packed + (size_t)r * kw;
+                uint32_t par = ib[(r >> 5) * kTile + lane] >> (r & 31);
+#pragma unroll
+                for (int w = 0; w < kTKW; ++w)
+                    if (w < kw) par += __builtin_popcount(ar[w] & zr[w]);
+                acc |= par & 1u;
+            }
+        }
+        if (acc) atomicOr((uint32_t *)bad + lane, 1u);
+        __syncthreads();
+
+        if (wave == 0) {  // per-lane exits and counters (vn_kernel's stream variant)
+            unsigned long long v[7] = {0, 0, 0, 0, 0, 0, 0};
+            bool fin = false;
+            if (c.live) {
+                const int it = itl[lane];
+                const bool ok = bad[lane] == 0;  // Result.OK at this iteration (:231-241)
+                fin = ok || it == max_iter - 1;  // else DATA_TRANSFER_NOT_OK (:244-253)
+                if (fin) {
+                    int err = 0;
+                    if (!ok)  // main.py:130-138: u vs z^1 of a failed frame
+                        for (int w = 0; w < kw; ++w) err += __builtin_popcount(Ut[w * kTile] ^ zb[w * kTile + lane]);
+                    v[0] = 1;
+                    v[1] = ok ? 0 : 1;
+                    v[2] = (unsigned long long)err;
+                    v[3] = ok ? (unsigned long long)it : 0;
+                    v[4] = ok ? 1 : 0;
+                    v[5] = nllr ? (unsigned long long)cntl[lane] : 0;
+                    v[6] = (unsigned long long)(it + 1);
+                    livel[lane] = 0;
+                    want = true;
+                } else {
+                    itl[lane] = it + 1;
+                }
+                freshl[lane] = 0;
+            }
+            if (__ballot(fin) != 0ull) {
+#pragma unroll
+                for (int i = 0; i < 7; ++i) {
+                    const unsigned long long s = wave_sum(v[i]);
+                    if (lane == 0 && s) atomicAdd(&ctr[i], s);
+                }
+            }
+            bad[lane] = 0;
+            cntl[lane] = 0;
+        }
+        for (int i = threadIdx.x; i < mw * kTile; i += blockDim.x) ib[i] = 0u;
+        // zb is cleared (and reused as the u-bit stage) at the top of the loop
+    }
+}
 
 }  // namespace
 
@@ -718,6 +923,21 @@ bool use_tile(const DevGraph &g) {
         return e ? atoi(e) : -1;
     }();
     return force != 0 && tile_lds_bytes(g) > 0;
+}
+
+bool use_tile_stream(const DevGraph &g) {
+    const char *e = getenv("LDPC_TILE_STREAM");
+    return (!e || atoi(e) != 0) && tile64_lds_bytes(g) > 0;
+}
+
+hipError_t launch_tile_stream(const DevGraph &g, const DevState &st, int max_iter, bool nllr, uint64_t seed,
+                              int snr_point, double sigma, int64_t frame0, int64_t total, unsigned long long *next,
+                              unsigned long long *ctr, hipStream_t s) {
+    const size_t lds = tile64_lds_bytes(g);
+    if (!lds || !g.a_packed || !st.ubits || st.ntiles > st.nslots) return hipErrorInvalidValue;
+    tile_stream_kernel<<<st.ntiles, 64 * kTW, lds, s>>>(g, st, max_iter, nllr ? 1 : 0, g.col_idx, g.row_ptr,
+                                                        kAtanhCoef, seed, snr_point, sigma, frame0, total, next, ctr);
+    return hipGetLastError();
 }
 
 hipError_t launch_tile(const DevGraph &g, const DevState &st, int max_iter, bool nllr, hipStream_t s) {

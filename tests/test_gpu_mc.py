@@ -131,3 +131,24 @@ def test_stream_zero_frames(gpu_available):
     dec = _decoder("BCH_7_4_1_strip", 64)
     ctr = dec.mc_run(SEED, [oracle.sigma_for_snr(1.0)], 0, 0, 10)
     assert not ctr.any()
+
+
+# The streaming schedule on tile-capable graphs runs inside the tile-resident
+# decoder (tile_stream_kernel: per-lane refill between passes); LDPC_F_SPLIT
+# keeps the per-iteration CN/VN/refill loop.  Same frames, same counters.
+@pytest.mark.parametrize("code,cap,frames,T,snrs", [
+    ("wimax_576_0.5", 192, 1000, 12, (0.0, 2.0, 3.5)),
+    ("wimax_576_0.5", 64, 333, 50, (2.5,)),
+    ("BCH_7_4_1_strip", 64, 5000, 10, (0.0, 4.0)),
+])
+def test_tile_stream_equals_split_stream(gpu_available, code, cap, frames, T, snrs):
+    dec = _decoder(code, cap)
+    sig = [oracle.sigma_for_snr(s) for s in snrs]
+    dec.profile(True)
+    a = dec.mc_run(SEED, sig, frames, 3, T, nllr=True)
+    p = dec.profile_read()
+    dec.profile(False)
+    assert p["tile"][1] == len(snrs) and p["cn"][1] == 0, p  # one tile launch per point
+    b = dec.mc_run(SEED, sig, frames, 3, T, nllr=True, split=True)
+    np.testing.assert_array_equal(a, b)
+    assert (a[:, 0] == frames).all()
