@@ -69,6 +69,7 @@ struct ldpc_decoder {
     int pactive_cap = 0;
     unsigned long long *counters = nullptr;  // [counters_cap] + 1 frame-index counter (streaming)
     int counters_cap = 0;
+    int *cpairs = nullptr;  // streaming tail compaction plan (1 + 2 cap ints), on first use
     DevState st{};
     // profiling (ldpc_profile_*)
     bool prof = false;
@@ -483,6 +484,7 @@ int ldpc_decoder_destroy(ldpc_decoder *d) {
     (void)hipFree(d->E);
     (void)hipFree(d->T);
     (void)hipFree(d->rare);
+    (void)hipFree(d->cpairs);
     (void)hipFree(d->L);
     (void)hipFree(d->ch);
     (void)hipFree(d->ints);
@@ -694,7 +696,7 @@ int mc_stream_point(ldpc_decoder *d, uint64_t seed, int p, double sigma, int64_t
     const DevGraph &G = d->g->dg;
     const int ntiles = (int)std::min<int64_t>(d->cap_tiles, (total + kTile - 1) / kTile);
     state_bind(d, ntiles, ntiles * kTile);
-    const DevState st = d->st;
+    DevState st = d->st;
     unsigned long long *ctr = d->counters + (size_t)p * LDPC_MC_NCOUNT;
     unsigned long long *next = d->counters + d->counters_cap;
     if (!split && ldpc::use_tile_stream(G) && st.ntiles <= st.nslots) {
@@ -718,6 +720,11 @@ int mc_stream_point(ldpc_decoder *d, uint64_t seed, int p, double sigma, int64_t
     const int64_t max_steps = (min_steps + 1) * (int64_t)max_iter;   // every frame stops by max_iter
     constexpr int kPoll = 4;
     int64_t step = 0;
+    const bool compact = [] {
+        const char *e = getenv("LDPC_COMPACT");
+        return !e || atoi(e) != 0;
+    }();
+    int cur = ntiles;  // tiles the steps launch (shrinks as the tail is compacted)
     for (;;) {
         // every frame fits in the slots: all start now and stop by max_iter
         const int64_t until = total <= slots ? std::max<int64_t>(step + kPoll, max_iter)
@@ -729,10 +736,23 @@ int mc_stream_point(ldpc_decoder *d, uint64_t seed, int p, double sigma, int64_t
             HIP_TRY(timed(d, LDPC_K_VN, s, [&] { return ldpc::launch_vn(G, st, 0, max_iter, nllr, s, ctr); }));
             HIP_TRY(refill());
         }
-        unsigned long long finished = 0;
+        unsigned long long finished = 0, handed = 0;
         HIP_TRY(hipMemcpyAsync(&finished, ctr, sizeof(finished), hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipMemcpyAsync(&handed, next, sizeof(handed), hipMemcpyDeviceToHost, s));
         HIP_TRY(hipStreamSynchronize(s));
         if ((int64_t)finished >= total) return LDPC_OK;
+        // tail: the supply is out and at most half of the launched slots
+        // still run -> move them into the first tiles and launch only those
+        const int64_t live = std::min<int64_t>((int64_t)handed, total) - (int64_t)finished;
+        if (compact && (int64_t)handed >= total && cur > 1 && live > 0 && live * 2 <= (int64_t)cur * kTile) {
+            const int nt = (int)((live + kTile - 1) / kTile);
+            const int cap = d->cap_tiles * kTile;
+            if (!d->cpairs && dev_alloc(&d->cpairs, 1 + 2 * (size_t)cap)) return LDPC_ENOMEM;
+            HIP_TRY(ldpc::launch_compact(G, st, nt, cap, d->cpairs, s));
+            state_bind(d, nt, nt * kTile);
+            st = d->st;
+            cur = nt;
+        }
         if (step > max_steps)
             return ldpc_fail(LDPC_EDEVICE, "ldpc_mc_run: streaming schedule did not drain (%llu of %lld frames)",
                              finished, (long long)total);

@@ -93,6 +93,9 @@ hipError_t launch_tile_sub(const DevGraph &g, const DevState &st, int max_iter, 
 hipError_t launch_stream_init(const DevGraph &g, const DevState &st, hipStream_t s);
 hipError_t launch_refill(const DevGraph &g, const DevState &st, uint64_t seed, int snr_point, double sigma,
                          int64_t frame0, int64_t total, unsigned long long *next, hipStream_t s);
+// streaming tail: move the frames running in tiles >= nt into finished slots
+// of tiles < nt (pairs: 1 + 2 cap ints of scratch)
+hipError_t launch_compact(const DevGraph &g, const DevState &st, int nt, int cap, int *pairs, hipStream_t s);
 hipError_t launch_finalize(const DevGraph &g, const DevState &st, uint8_t *z, double *post,
                            hipStream_t s);
 hipError_t launch_export_msgs(const DevGraph &g, const DevState &st, double *out, hipStream_t s);

@@ -738,6 +738,111 @@ hipError_t launch_refill(const DevGraph &g, const DevState &st, uint64_t seed, i
     return hipGetLastError();
 }
 
+// ------------------------------------------------ streaming tail compaction
+// Once the frame supply is out, the frames still running are scattered over
+// every tile and each step still costs every tile they touch.  Frames running
+// in tiles >= nt move into finished slots of tiles < nt (sources and
+// destinations are disjoint: no ordering hazard); the steps after that launch
+// nt tiles.  A frame's state is its lane of E, L, ch, ubits and its iters /
+// fresh flags -- it decodes exactly as before, so the counters do not change.
+// plan (one workgroup): pairs[0] = P, pairs[1..P] sources, pairs[1+cap..] destinations
+__global__ __launch_bounds__(1024) void compact_plan_kernel(DevState st, int nt, int cap, int *pairs) {
+    __shared__ int sa[1024], sb[1024];
+    const int slots = st.ntiles * kTile, low = nt * kTile;
+    const int per = (slots + blockDim.x - 1) / blockDim.x;
+    const int b0 = threadIdx.x * per, b1 = min(slots, b0 + per);
+    int na = 0, nb = 0;  // live in the high tiles, finished in the low tiles
+    for (int f = b0; f < b1; ++f) {
+        const bool live = st.done[f] == 0;
+        na += (f >= low && live) ? 1 : 0;
+        nb += (f < low && !live) ? 1 : 0;
+    }
+    sa[threadIdx.x] = na;
+    sb[threadIdx.x] = nb;
+    __syncthreads();
+    for (int o = 1; o < (int)blockDim.x; o <<= 1) {  // inclusive scans
+        const int va = threadIdx.x >= (unsigned)o ? sa[threadIdx.x - o] : 0;
+        const int vb = threadIdx.x >= (unsigned)o ? sb[threadIdx.x - o] : 0;
+        __syncthreads();
+        sa[threadIdx.x] += va;
+        sb[threadIdx.x] += vb;
+        __syncthreads();
+    }
+    int ia = sa[threadIdx.x] - na, ib = sb[threadIdx.x] - nb;
+    const int P = min(sa[blockDim.x - 1], sb[blockDim.x - 1]);
+    for (int f = b0; f < b1; ++f) {
+        const bool live = st.done[f] == 0;
+        if (f >= low && live) {
+            if (ia < P) pairs[1 + ia] = f;
+            ++ia;
+        } else if (f < low && !live) {
+            if (ib < P) pairs[1 + cap + ib] = f;
+            ++ib;
+        }
+    }
+    if (threadIdx.x == 0) pairs[0] = P;
+}
+
+// move: every (pair, item) of E / L / ch / ubits
+__global__ void compact_move_kernel(DevGraph g, DevState st, int cap, const int *pairs) {
+    const int P = pairs[0];
+    const int kw = (g.k + 31) >> 5;
+    const int64_t items = (int64_t)g.nnz + 2 * (int64_t)g.n + kw;
+    const int64_t total = (int64_t)P * items;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+        const int p = (int)(i / items);
+        int64_t it = i % items;
+        const int src = pairs[1 + p], dst = pairs[1 + cap + p];
+        const size_t st_ = src >> 6, sl = src & 63, dt = dst >> 6, dl = dst & 63;
+        if (it < g.nnz) {
+            st.E[(dt * g.nnz + it) * kTile + dl] = st.E[(st_ * g.nnz + it) * kTile + sl];
+            continue;
+        }
+        it -= g.nnz;
+        if (it < g.n) {
+            st.L[(dt * g.n + it) * kTile + dl] = st.L[(st_ * g.n + it) * kTile + sl];
+            continue;
+        }
+        it -= g.n;
+        if (it < g.n) {
+            st.ch[(dt * g.n + it) * kTile + dl] = st.ch[(st_ * g.n + it) * kTile + sl];
+            continue;
+        }
+        it -= g.n;
+        st.ubits[(dt * kw + it) * kTile + dl] = st.ubits[(st_ * kw + it) * kTile + sl];
+    }
+}
+
+__global__ void compact_flags_kernel(DevState st, int cap, const int *pairs) {
+    const int p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= pairs[0]) return;
+    const int src = pairs[1 + p], dst = pairs[1 + cap + p];
+    st.done[dst] = 0;
+    st.refill[dst] = 0;
+    st.iters[dst] = st.iters[src];
+    st.fresh[dst] = st.fresh[src];
+    st.done[src] = 1;
+    st.refill[src] = 0;
+    st.fresh[src] = 0;
+}
+
+__global__ void tile_active_kernel(DevState st) {  // after a compaction: which of the nt tiles run
+    const int tile = blockIdx.x;
+    const int lane = threadIdx.x;
+    const unsigned long long busy = __ballot(st.done[tile * kTile + lane] == 0);
+    if (lane == 0) st.tile_active[tile] = busy != 0ull ? 1 : 0;
+}
+
+hipError_t launch_compact(const DevGraph &g, const DevState &st, int nt, int cap, int *pairs, hipStream_t s) {
+    compact_plan_kernel<<<1, 1024, 0, s>>>(st, nt, cap, pairs);
+    compact_move_kernel<<<2048, 256, 0, s>>>(g, st, cap, pairs);
+    compact_flags_kernel<<<grid_for(cap, 256), 256, 0, s>>>(st, cap, pairs);
+    DevState lo = st;
+    lo.ntiles = nt;
+    tile_active_kernel<<<nt, kTile, 0, s>>>(lo);
+    return hipGetLastError();
+}
+
 hipError_t launch_finalize(const DevGraph &g, const DevState &st, uint8_t *z, double *post, hipStream_t s) {
     const size_t total = (size_t)st.count * g.n;
     if (total) finalize_kernel<<<grid_for(total, 256), 256, 0, s>>>(g, st, z, post);

@@ -152,3 +152,20 @@ def test_tile_stream_equals_split_stream(gpu_available, code, cap, frames, T, sn
     b = dec.mc_run(SEED, sig, frames, 3, T, nllr=True, split=True)
     np.testing.assert_array_equal(a, b)
     assert (a[:, 0] == frames).all()
+
+
+def test_stream_tail_compaction_keeps_counters(gpu_available, monkeypatch):
+    """The split streaming schedule compacts its tail (frames still running once
+    the supply is out move into the first tiles): counters equal the
+    uncompacted stream and the static schedule."""
+    code, cap, frames, T = "wimax_2304_0.5", 256, 1500, 20
+    dec = _decoder(code, cap)
+    sig = [oracle.sigma_for_snr(s) for s in (2.5, 3.0)]
+    a = dec.mc_run(SEED, sig, frames, 11, T, nllr=True)
+    monkeypatch.setenv("LDPC_COMPACT", "0")
+    b = dec.mc_run(SEED, sig, frames, 11, T, nllr=True)
+    monkeypatch.delenv("LDPC_COMPACT")
+    c = dec.mc_run(SEED, sig, frames, 11, T, nllr=True, static=True)
+    np.testing.assert_array_equal(a, b)
+    np.testing.assert_array_equal(a, c)
+    assert (a[:, 0] == frames).all()
