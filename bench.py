@@ -278,6 +278,8 @@ def main():
     tile_ms, tile_launches = prof.get("tile", (0.0, 0))
     if tile_launches:  # tile-resident decoder: one launch decodes a chunk through all its iterations
         cn_name = _lib.lib().ldpc_tile_kernel_name(graph.handle).decode() or "tile_kernel"
+        if args.schedule == "stream" and cn_name == "tile_kernel":
+            cn_name = "tile_stream_kernel"  # the streaming Monte-Carlo variant of the same decoder
         decode_ms = tile_ms
         decode_gbs = dec_bytes / (decode_ms / 1e3) / 1e9 if decode_ms else 0.0
     out = {
