@@ -41,7 +41,9 @@ def parse():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--code", default="wimax_576_0.5")
     ap.add_argument("--frames", type=int, default=65536, help="frames per GPU per step")
-    ap.add_argument("--chunk", type=int, default=0, help="decoder slots (frames resident at once); 0 = whole batch")
+    ap.add_argument("--chunk", type=int, default=0,
+                    help="decoder slots (frames resident at once); 0 = whole batch, capped by an HBM budget "
+                         "(Decoder.fit_slots, LDPC_HBM_BUDGET_GB, default 160)")
     ap.add_argument("--schedule", choices=("auto", "stream", "static"), default="auto",
                     help="stream: a slot takes the next frame as soon as its frame stops; static: chunks decoded "
                          "to completion (same frames, same counters); auto: static where the tile-resident "
@@ -215,7 +217,7 @@ def main():
         graph = Graph(H, device=local)
         Hphys = edd.physical_matrix() if args.mode == "physical" else None
         pgraph = Graph(Hphys, device=local) if Hphys is not None else None
-    chunk = args.chunk or args.frames
+    chunk = args.chunk or Decoder.fit_slots(graph, args.frames)  # whole batch, if its state fits the HBM budget
     dec = Decoder(graph, chunk)
     if args.schedule == "auto":
         from ldpc_amd import _lib

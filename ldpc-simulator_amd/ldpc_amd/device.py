@@ -7,6 +7,7 @@
 """
 import ctypes
 import hashlib
+import os
 import threading
 
 import numpy as np
@@ -101,6 +102,26 @@ class Decoder:
     @staticmethod
     def workspace_bytes(graph, max_frames):
         return int(_lib.lib().ldpc_decoder_bytes(graph.handle, int(max_frames)))
+
+    # HBM the Monte-Carlo drivers let one decoder take (of 288 GB per MI355X);
+    # LDPC_HBM_BUDGET_GB overrides
+    HBM_BUDGET = 160e9
+
+    @classmethod
+    def fit_slots(cls, graph, frames, budget=None):
+        """Slots (resident frames, a multiple of 64) for a workspace of at most
+        `budget` bytes, and no more than `frames`: fp64 messages are 8 B per
+        edge per frame, 5.3 MB for wimax_2304_0.5, so its 65,536-frame batch
+        (348 GB) streams through ~30k slots instead."""
+        if budget is None:
+            budget = float(os.environ.get("LDPC_HBM_BUDGET_GB", cls.HBM_BUDGET / 1e9)) * 1e9
+        # workspace = fixed (rare-row scratch, graph-sized buffers) + per-frame state
+        a, b = 64 * 64, 2 * 64 * 64
+        wa, wb = cls.workspace_bytes(graph, a), cls.workspace_bytes(graph, b)
+        per = (wb - wa) / (b - a)
+        fixed = wa - per * a
+        fit = max(64, int((budget - fixed) // per) // 64 * 64)
+        return max(1, min(int(frames), fit))
 
     def decode(self, llr, max_iter, nllr=False, post=False, hist=False, msgs=False, split=False):
         """Decode [B, n] channel LLRs (H_std column order).  Returns numpy arrays.

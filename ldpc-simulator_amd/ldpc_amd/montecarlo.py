@@ -116,7 +116,7 @@ def simulate(matrix, snrs, blocks, max_iter, seed=20260213, nllr=False, chunk=65
     else:
         edd = load_committed_code(matrix)
     g = Graph(edd._h_std, device=device)
-    dec = Decoder(g, min(max(1, shard(int(blocks), rank, world)[1]), chunk))
+    dec = Decoder(g, Decoder.fit_slots(g, min(max(1, shard(int(blocks), rank, world)[1]), chunk)))
     ctr = run_sweep(dec, snrs, blocks, max_iter, seed=seed, nllr=nllr, rank=rank, world=world,
                     allreduce=allreduce)
     pts = point_results(ctr, edd._k, snrs, matrix_path=matrix_path or str(matrix), max_iter=max_iter)

@@ -169,3 +169,18 @@ def test_stream_tail_compaction_keeps_counters(gpu_available, monkeypatch):
     np.testing.assert_array_equal(a, b)
     np.testing.assert_array_equal(a, c)
     assert (a[:, 0] == frames).all()
+
+
+def test_fit_slots_caps_the_workspace(gpu_available):
+    """A batch whose fp64 state exceeds the HBM budget streams through fewer
+    slots (wimax_2304_0.5: 5.3 MB per frame)."""
+    from ldpc_amd.device import Decoder, Graph
+    g = Graph.cached(hstd_for("wimax_2304_0.5"))
+    assert Decoder.fit_slots(g, 65536) < 65536  # 348 GB of messages > the 160 GB default
+    slots = Decoder.fit_slots(g, 65536, budget=3e9)
+    assert slots % 64 == 0 and 64 <= slots < 1024
+    assert Decoder.workspace_bytes(g, slots) <= 3e9
+    assert Decoder.fit_slots(Graph.cached(hstd_for("wimax_576_0.5")), 65536) == 65536
+    dec = Decoder(g, slots)
+    ctr = dec.mc_run(SEED, [oracle.sigma_for_snr(3.0)], 3 * slots + 5, 0, 6)
+    assert ctr[0, 0] == 3 * slots + 5
