@@ -927,7 +927,9 @@ bool use_tile(const DevGraph &g) {
 
 bool use_tile_stream(const DevGraph &g) {
     const char *e = getenv("LDPC_TILE_STREAM");
-    return (!e || atoi(e) != 0) && tile64_lds_bytes(g) > 0;
+    const size_t lds = tile64_lds_bytes(g);
+    // + the kernel's static per-lane state (itl, freshl: 2 x 64 ints)
+    return (!e || atoi(e) != 0) && lds > 0 && lds + 2 * kTile * sizeof(int) <= kTileLdsMax;
 }
 
 hipError_t launch_tile_stream(const DevGraph &g, const DevState &st, int max_iter, bool nllr, uint64_t seed,
