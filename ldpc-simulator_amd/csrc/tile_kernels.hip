@@ -153,8 +153,8 @@ constexpr int kTG = LDPC_TILE_GROUP;
 // LDPC_TILE_TRACE (diagnostic build): s_memtime stamps of every wavefront of
 // workgroup 0 at the phase boundaries of rows 0..kTrRows-1 of pass 2, read
 // back with ldpc_diag_tile_trace (ldpc_api.cpp); tools/tile_trace.py.
-constexpr int kTrRows = 64, kTrEv = 8;
 #ifdef LDPC_TILE_TRACE
+constexpr int kTrRows = 64, kTrEv = 8;
 __device__ unsigned long long g_tile_trace[kTW][kTrRows][kTrEv];
 #define TSTAMP(c, r, ev)                                                                              \
     do {                                                                                              \
