@@ -140,6 +140,8 @@ def test_stream_zero_frames(gpu_available):
     ("wimax_576_0.5", 192, 1000, 12, (0.0, 2.0, 3.5)),
     ("wimax_576_0.5", 64, 333, 50, (2.5,)),
     ("BCH_7_4_1_strip", 64, 5000, 10, (0.0, 4.0)),
+    ("wimax_576_0.5", 128, 130, 1, (1.0, 6.0)),     # max_iter 1: every frame stops after its first pass
+    ("wimax_576_0.5", 4096, 70, 8, (0.5,)),         # far fewer frames than slots (idle workgroups)
 ])
 def test_tile_stream_equals_split_stream(gpu_available, code, cap, frames, T, snrs):
     dec = _decoder(code, cap)
