@@ -73,6 +73,20 @@ inline size_t cn_lds_pad() {
 }
 constexpr int kPf = LDPC_PF;  // edges in flight per wavefront (software pipeline depth)
 
+// LDPC_SPLIT_NT 1: the message array E (streamed once per pass, far larger
+// than L2) is loaded and stored non-temporally by the CN/VN kernels, so it
+// does not evict the tiles' posteriors (the L[col] gather) from L2.
+#ifndef LDPC_SPLIT_NT
+#define LDPC_SPLIT_NT 1
+#endif
+__device__ __forceinline__ double ld_e(const double *p) { return LDPC_SPLIT_NT ? __builtin_nontemporal_load(p) : *p; }
+__device__ __forceinline__ void st_e(double *p, double v) {
+    if (LDPC_SPLIT_NT)
+        __builtin_nontemporal_store(v, p);
+    else
+        *p = v;
+}
+
 // Register ring of the next kPf edges' (L[col], E_old) loads.  take(k, e)
 // returns M for edge e (ring slot k) and issues the loads for edge e + kPf.
 // kStream (streaming Monte-Carlo): a lane whose frame was just loaded
@@ -96,7 +110,7 @@ struct EdgeStream {
         // keeps the ring in place and waits only for the slot it consumes
         const int i = e < end ? e : end - 1;
         lv[k] = Lt[col[i] * kTile];  // col[] is read-only + noalias -> scalar load
-        eo[k] = kFirst ? 0.0 : Et[i * kTile];
+        eo[k] = kFirst ? 0.0 : ld_e(&Et[i * kTile]);
     }
     __device__ __forceinline__ double take(int k, int e) {
         const double M = kFirst ? lv[k] : lv[k] - ((kStream && fresh) ? 0.0 : eo[k]);
@@ -168,7 +182,7 @@ __global__ __launch_bounds__(256, LDPC_CN_WAVES) void cn_kernel(DevGraph g, DevS
 #else
                     const double En = 2.0 * atanh_f(clip_cl(P / t), ltab, ac);
 #endif
-                    if (live) Et[(e + k) * kTile] = En;
+                    if (live) st_e(&Et[(e + k) * kTile], En);
                 }
             }
         }
@@ -248,7 +262,7 @@ __global__ __launch_bounds__(64 * kRowW, WPS) void cn_row_kernel(DevGraph g, Dev
             for (int i = h * H; i < (h + 1) * H; ++i) {
                 const int e = c0 + min(i, cnt - 1);
                 t[i] = Lt[col_idx[e] * kTile];
-                eo[i - h * H] = kFirst ? 0.0 : Et[e * kTile];
+                eo[i - h * H] = kFirst ? 0.0 : ld_e(&Et[e * kTile]);
             }
 #pragma unroll
             for (int i = h * H; i < (h + 1) * H; ++i) {
@@ -286,7 +300,7 @@ __global__ __launch_bounds__(64 * kRowW, WPS) void cn_row_kernel(DevGraph g, Dev
 #else
             const double En = 2.0 * atanh_f(clip_cl(P / t[i]), ltab, ac);
 #endif
-            if (live) Et[(c0 + i) * kTile] = En;
+            if (live) st_e(&Et[(c0 + i) * kTile], En);
         }
     }
 }
@@ -394,12 +408,12 @@ __global__ __launch_bounds__(1024) void vn_kernel(DevGraph g, DevState st, int i
             // ring of kPv loads in flight (indices clamped into the column)
             double ring[kPv];
 #pragma unroll
-            for (int k = 0; k < kPv; ++k) ring[k] = Et[csc_edge[min(p0 + k, p1 - 1)] * kTile];
+            for (int k = 0; k < kPv; ++k) ring[k] = ld_e(&Et[csc_edge[min(p0 + k, p1 - 1)] * kTile]);
             for (int p = p0; p < p1; p += kPv) {
 #pragma unroll
                 for (int k = 0; k < kPv; ++k) {
                     const double v = ring[k];
-                    ring[k] = Et[csc_edge[min(p + k + kPv, p1 - 1)] * kTile];
+                    ring[k] = ld_e(&Et[csc_edge[min(p + k + kPv, p1 - 1)] * kTile]);
                     if (p + k < p1) s = s + v;
                 }
             }

@@ -149,6 +149,22 @@ constexpr int kTG = LDPC_TILE_GROUP;
 #ifndef LDPC_TILE_CONST_COEF
 #define LDPC_TILE_CONST_COEF 0
 #endif
+//   LDPC_TILE_NT        bit 0: E_old loads, bit 1: E_new stores as non-temporal
+//                       accesses: the message stream (read once, written once
+//                       per iteration) then does not evict the tile's
+//                       posteriors (the L[col] gather) from L2
+#ifndef LDPC_TILE_NT
+#define LDPC_TILE_NT 3
+#endif
+__device__ __forceinline__ double ld_msg(const double *p) {
+    return (LDPC_TILE_NT & 1) ? __builtin_nontemporal_load(p) : *p;
+}
+__device__ __forceinline__ void st_msg(double *p, double v) {
+    if (LDPC_TILE_NT & 2)
+        __builtin_nontemporal_store(v, p);
+    else
+        *p = v;
+}
 
 // LDPC_TILE_TRACE (diagnostic build): s_memtime stamps of every wavefront of
 // workgroup 0 at the phase boundaries of rows 0..kTrRows-1 of pass 2, read
@@ -229,7 +245,7 @@ __device__ __forceinline__ double tile_load_e(const TileCtx &c, const RowChunk &
 #ifdef LDPC_TILE_DIAG_NOLOAD_E
     return (double)(int)(c.lane + i) * 0.0625;
 #endif
-    return c.first ? 0.0 : *at(c.Eb, rc.c0 + min(i, rc.cnt - 1), c.lane);
+    return c.first ? 0.0 : ld_msg(at(c.Eb, rc.c0 + min(i, rc.cnt - 1), c.lane));
 }
 __device__ __forceinline__ bool tile_t(const TileCtx &c, double &t, double eo) {
     const double M = c.first ? t : t - (c.fresh ? 0.0 : eo);  // :85-90 / :260-268
@@ -461,7 +477,7 @@ __device__ __forceinline__ void tile_p3(TileCtx &c, int r, double (&t)[kTK], con
     if (store1 && c.live) {  // the chunk's E_new stores under ONE exec mask
 #pragma unroll
         for (int i = 0; i < kTK; ++i)
-            if (i < rc.cnt) *at(c.Eb, rc.c0 + i, c.lane) = t[i];
+            if (i < rc.cnt) st_msg(at(c.Eb, rc.c0 + i, c.lane), t[i]);
     }
 #pragma unroll
     for (int i = 0; i < kTK; ++i) {
@@ -469,7 +485,7 @@ __device__ __forceinline__ void tile_p3(TileCtx &c, int r, double (&t)[kTK], con
             if (fused) t[i] = 2.0 * atanh_f(clip_cl(P / t[i]), c.ltab, c.ac);  // :159-168
             const int e = rc.c0 + i;
             const int col = c.col_idx[e];
-            if (!store1 && c.live) *at(c.Eb, e, c.lane) = t[i];
+            if (!store1 && c.live) st_msg(at(c.Eb, e, c.lane), t[i]);
             if (col < c.k) {  // S_col += E (rows ascending)
                 double *sp = c.S + col * kTile + c.lane;
                 *sp = *sp + t[i];
