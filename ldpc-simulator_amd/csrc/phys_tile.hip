@@ -33,6 +33,21 @@
 namespace ldpc {
 namespace {
 
+// LDPC_PHYS_NT 1: the fp32 message array (streamed once per pass in each
+// direction, far larger than L2) is loaded / stored non-temporally, so the
+// gathers of L keep L2 to themselves (as the parity kernels' E stream).
+#ifndef LDPC_PHYS_NT
+#define LDPC_PHYS_NT 1
+#endif
+__device__ __forceinline__ float ld_e32(const float *p) { return LDPC_PHYS_NT ? __builtin_nontemporal_load(p) : *p; }
+__device__ __forceinline__ void st_e32(float *p, float v) {
+    if (LDPC_PHYS_NT)
+        __builtin_nontemporal_store(v, p);
+    else
+        *p = v;
+}
+
+
 constexpr int kRowsPerWave = 4;
 constexpr int kColsPerWave = 8;
 
@@ -110,7 +125,7 @@ __global__ __launch_bounds__(256) void phys_cn_tile_kernel(DevGraph g, DevState 
                     const float Lc = live ? Lt[col_idx[beg + i] * kTile] : 0.0f;
                     hp ^= Lc < 0.0f ? 1u : 0u;
                     if (!syn_only) {
-                        const float M = (first || !live) ? Lc : Lc - Et[(beg + i) * kTile];
+                        const float M = (first || !live) ? Lc : Lc - ld_e32(&Et[(beg + i) * kTile]);
                         ph[i] = phi(fabsf(M));
                         S += ph[i];
                         sg |= (M < 0.0f ? 1u : 0u) << i;
@@ -123,7 +138,7 @@ __global__ __launch_bounds__(256) void phys_cn_tile_kernel(DevGraph g, DevState 
                 for (int i = 0; i < kDeg; ++i) {
                     if (i < deg) {
                         const float mag = phi(fmaxf(S - ph[i], 0.0f));
-                        Et[(beg + i) * kTile] = ((neg ^ (sg >> i)) & 1u) ? -mag : mag;
+                        st_e32(&Et[(beg + i) * kTile], ((neg ^ (sg >> i)) & 1u) ? -mag : mag);
                     }
                 }
             }
@@ -142,9 +157,9 @@ __global__ __launch_bounds__(256) void phys_cn_tile_kernel(DevGraph g, DevState 
             if (upd) {
                 for (int e = beg; e < end; ++e) {
                     const float Lc = Lt[col_idx[e] * kTile];
-                    const float M = first ? Lc : Lc - Et[e * kTile];
+                    const float M = first ? Lc : Lc - ld_e32(&Et[e * kTile]);
                     const float mag = phi(fmaxf(S - phi(fabsf(M)), 0.0f));
-                    Et[e * kTile] = ((neg ^ ((M < 0.0f) ? 1u : 0u)) != 0u) ? -mag : mag;
+                    st_e32(&Et[e * kTile], ((neg ^ ((M < 0.0f) ? 1u : 0u)) != 0u) ? -mag : mag);
                 }
             }
         }
@@ -178,7 +193,7 @@ __global__ __launch_bounds__(256) void phys_vn_tile_kernel(DevGraph g, DevState 
         for (int j = j0; j < j1; ++j) {
             if (upd) {  // lane-masked: converged / finished frames move no data
                 float s = Lamt[j * kTile];
-                for (int p = csc_ptr[j]; p < csc_ptr[j + 1]; ++p) s += Et[csc_edge[p] * kTile];
+                for (int p = csc_ptr[j]; p < csc_ptr[j + 1]; ++p) s += ld_e32(&Et[csc_edge[p] * kTile]);
                 Lt[j * kTile] = s;
             }
         }
