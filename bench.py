@@ -71,7 +71,10 @@ def dist_setup(args):
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
     device = local
-    if world > 1:
+    # LDPC_BENCH_FORCE_DIST=1: the N>1 code path (torch first, RCCL process
+    # group, counter all-reduce, max over ranks) with a single rank -- how the
+    # driver's multi-GPU run is rehearsed on a one-GPU box
+    if world > 1 or os.environ.get("LDPC_BENCH_FORCE_DIST") == "1":
         import torch
         import torch.distributed as dist
         device = local % max(1, torch.cuda.device_count())

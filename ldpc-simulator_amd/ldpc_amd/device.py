@@ -14,7 +14,8 @@ import numpy as np
 from scipy import sparse
 
 from . import _lib
-from ._lib import LDPC_F_NLLR, LDPC_F_PHYS_HBM, LDPC_F_SPLIT, LDPC_F_STATIC, LDPC_MC_NCOUNT, as_i32, check
+from ._lib import (LDPC_F_DEVICE_PTRS, LDPC_F_NLLR, LDPC_F_PHYS_HBM, LDPC_F_SPLIT, LDPC_F_STATIC, LDPC_MC_NCOUNT,
+                   as_i32, check)
 
 
 def _csr_arrays(H):
@@ -149,6 +150,25 @@ class Decoder:
             self._h, B, _lib.ptr(llr), T, flags, _lib.ptr(z), _lib.ptr(conv), _lib.ptr(status),
             _lib.ptr(Lp), _lib.ptr(nl), _lib.ptr(hi), _lib.ptr(iters), _lib.ptr(E), None))
         return DecodeResult(z=z, conv=conv, status=status, iters=iters, nllr=nl, post=Lp, hist=hi, msgs=E)
+
+    def decode_device(self, llr, max_iter, z=None, conv=None, status=None, post=None, nllr=None, hist=None,
+                      iters=None, split=False, stream=None):
+        """LDPC_F_DEVICE_PTRS: every buffer is device memory (anything with a
+        data_ptr(), e.g. a torch CUDA tensor: llr [B, n] f64, z [B, n] u8,
+        conv / status / iters [B] i32, post [B, n] f64, nllr [B] f64, hist
+        [B, max_iter] f64), and the call is asynchronous on `stream` (a
+        hipStream_t handle as int; None = the null stream) unless nllr or hist
+        is requested.  Same results as decode()."""
+        def dp(t):
+            return None if t is None else ctypes.c_void_p(int(t.data_ptr()))
+        B, n = int(llr.shape[0]), int(llr.shape[1])
+        if n != self.graph.n:
+            raise ValueError(f"llr must be [batch, {self.graph.n}]")
+        flags = LDPC_F_DEVICE_PTRS | (LDPC_F_NLLR if (nllr is not None or hist is not None) else 0) | \
+            (LDPC_F_SPLIT if split else 0)
+        check("ldpc_decode_f64", _lib.lib().ldpc_decode_f64(
+            self._h, B, dp(llr), int(max_iter), flags, dp(z), dp(conv), dp(status), dp(post), dp(nllr), dp(hist),
+            dp(iters), None, ctypes.c_void_p(int(stream)) if stream else None))
 
     def generate(self, seed, snr_point, sigma, frame0, count):
         """On-device synthetic frames (u bits, channel LLRs) copied back for testing."""
