@@ -19,6 +19,30 @@ __device__ __forceinline__ int uniform(int x) { return __builtin_amdgcn_readfirs
 // be for finite or infinite channel LLRs (|t| <= 1, |E| <= 35.04).
 __device__ __forceinline__ double clip_cl(double q) { return fmin(fmax(q, -kCL), kCL); }
 
+// P / t as the compiler's own f64 division sequence (reciprocal, two Newton
+// steps, quotient, one fma correction -- the operations v_div_fmas_f64 and
+// v_div_fixup_f64 wrap) without v_div_scale_f64 / v_div_fmas / v_div_fixup.
+// Those only act on operands that need scaling or on special values, so the
+// result is the IEEE quotient, bit for bit, whenever t is normal with
+// |t| < 1 (every t of a non-rare row: 1e-10 < |t| <= CL) and |P| >= 2^-900
+// (callers check the latter per wavefront and divide normally otherwise).
+// LDPC_DIV_NR 0 keeps the plain division everywhere.
+#ifndef LDPC_DIV_NR
+#define LDPC_DIV_NR 1
+#endif
+constexpr double kDivNrMin = 0x1p-900;
+__device__ __forceinline__ double div_nr(double P, double t) {
+    const double r0 = __builtin_amdgcn_rcp(t);
+    const double r1 = __builtin_fma(r0, __builtin_fma(-t, r0, 1.0), r0);
+    const double r2 = __builtin_fma(r1, __builtin_fma(-t, r1, 1.0), r1);
+    const double q = P * r2;
+    return __builtin_fma(__builtin_fma(-t, q, P), r2, q);
+}
+// whether every lane of the wavefront may take div_nr for numerator P
+__device__ __forceinline__ bool div_nr_ok(double P) {
+    return LDPC_DIV_NR && __ballot(!(__builtin_fabs(P) >= kDivNrMin)) == 0ull;
+}
+
 // ---- math tables in LDS (9 x 16 tanh pairs + 128 log entries = 6.4 KB)
 struct LdsTanh {
     const Pair *p;

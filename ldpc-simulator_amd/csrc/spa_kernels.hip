@@ -171,6 +171,7 @@ __global__ __launch_bounds__(256, LDPC_CN_WAVES) void cn_kernel(DevGraph g, DevS
         // E_new = 2 atanh(clip(P/t)) written over E_old.  24 B of HBM per edge
         // instead of parking t (32 B).
         EdgeStream<kFirst, kStream> es(col_idx, Lt, Et, beg, end, fresh);
+        const bool nr = div_nr_ok(P);  // wave-uniform (cn_common.h)
         for (int e = beg; e < end; e += kPf) {
 #pragma unroll
             for (int k = 0; k < kPf; ++k) {
@@ -180,7 +181,7 @@ __global__ __launch_bounds__(256, LDPC_CN_WAVES) void cn_kernel(DevGraph g, DevS
 #ifdef LDPC_DIAG_NOMATH
                     const double En = P * t;
 #else
-                    const double En = 2.0 * atanh_f(clip_cl(P / t), ltab, ac);
+                    const double En = 2.0 * atanh_f(clip_cl(nr ? div_nr(P, t) : P / t), ltab, ac);
 #endif
                     if (live) st_e(&Et[(e + k) * kTile], En);
                 }
@@ -292,6 +293,16 @@ __global__ __launch_bounds__(64 * kRowW, WPS) void cn_row_kernel(DevGraph g, Dev
         __syncthreads();
     }
     const double P = chain[lane];
+    if (div_nr_ok(P)) {  // the IEEE quotient without the scaling steps (cn_common.h)
+#pragma unroll
+        for (int i = 0; i < K; ++i) {
+            if (i < cnt) {
+                const double En = 2.0 * atanh_f(clip_cl(div_nr(P, t[i])), ltab, ac);
+                if (live) st_e(&Et[(c0 + i) * kTile], En);
+            }
+        }
+        return;
+    }
 #pragma unroll
     for (int i = 0; i < K; ++i) {
         if (i < cnt) {
