@@ -144,6 +144,12 @@ __host__ __device__ inline TileLayout tile_layout(int k, int m) {
 #define LDPC_TILE_GROUP 1
 #endif
 constexpr int kTG = LDPC_TILE_GROUP;
+//   LDPC_TILE_DIVNR     P3's P / t as cn_common.h div_nr (bit-identical):
+//                       0 off, 1 per-wavefront branch around the group loop,
+//                       2 per-edge select between div_nr and P / t
+#ifndef LDPC_TILE_DIVNR
+#define LDPC_TILE_DIVNR 0
+#endif
 //   LDPC_TILE_CONST_COEF 1: atanh coefficients as compile-time constants
 //                       instead of kernel-argument SGPRs
 #ifndef LDPC_TILE_CONST_COEF
@@ -428,6 +434,25 @@ __device__ __forceinline__ void tile_p3(TileCtx &c, int r, double (&t)[kTK], con
 #pragma unroll
             for (int i = 0; i < kTK; ++i)
                 if (i < rc.cnt) t[i] = 2.0 * atanh_f(t[i], c.ltab, c.ac);
+        }
+    } else if (!tiny_row && !LDPC_TILE_P3FUSED && LDPC_TILE_DIVNR == 1 && div_nr_ok(P)) {
+#pragma unroll
+        for (int g0 = 0; g0 < kTK; g0 += kTG) {
+            if (g0 < rc.cnt) {
+#pragma unroll
+                for (int i = g0; i < min(g0 + kTG, kTK); ++i)
+                    t[i] = 2.0 * atanh_f(clip_cl(div_nr(P, t[i])), c.ltab, c.ac);  // :159-168
+            }
+        }
+    } else if (!tiny_row && !LDPC_TILE_P3FUSED && LDPC_TILE_DIVNR == 2) {
+        const bool nr = div_nr_ok(P);
+#pragma unroll
+        for (int g0 = 0; g0 < kTK; g0 += kTG) {
+            if (g0 < rc.cnt) {
+#pragma unroll
+                for (int i = g0; i < min(g0 + kTG, kTK); ++i)
+                    t[i] = 2.0 * atanh_f(clip_cl(nr ? div_nr(P, t[i]) : P / t[i]), c.ltab, c.ac);  // :159-168
+            }
         }
     } else if (!tiny_row && !LDPC_TILE_P3FUSED) {
 #pragma unroll
