@@ -17,7 +17,16 @@ __device__ __forceinline__ int uniform(int x) { return __builtin_amdgcn_readfirs
 // np.clip(q, -CL, CL) as v_max_f64 + v_min_f64 (2 VALU instead of 2 compares
 // and 4 selects).  Differs from np.clip only for NaN, which a message cannot
 // be for finite or infinite channel LLRs (|t| <= 1, |E| <= 35.04).
-__device__ __forceinline__ double clip_cl(double q) { return fmin(fmax(q, -kCL), kCL); }
+#ifndef LDPC_CLIP_ABS
+#define LDPC_CLIP_ABS 0
+#endif
+__device__ __forceinline__ double clip_cl(double q) {
+#if LDPC_CLIP_ABS  // |q| clipped, sign put back: one constant register pair instead of two
+    return __builtin_copysign(fmin(__builtin_fabs(q), kCL), q);
+#else
+    return fmin(fmax(q, -kCL), kCL);
+#endif
+}
 
 // P / t as the compiler's own f64 division sequence (reciprocal, two Newton
 // steps, quotient, one fma correction -- the operations v_div_fmas_f64 and

@@ -83,6 +83,9 @@ constexpr AtanhCoef kAtanhCoef{1.0 / 13.0, 1.0 / 11.0, 1.0 / 9.0, 1.0 / 7.0, 0.2
 
 // log(x) = hi + lo for a positive normal x.  Accurate away from x ~ 1 (the
 // interval holding 1.0 itself is exact: invc = 1), which is all atanh needs.
+#ifndef LDPC_L2_INLINE
+#define LDPC_L2_INLINE 0
+#endif
 template <class LogTab>
 __host__ __device__ __forceinline__ void log_hilo(double x, const LogTab &lt, double &hi, double &lo,
                                                   const AtanhCoef &c = kAtanhCoef) {
@@ -105,7 +108,11 @@ __host__ __device__ __forceinline__ void log_hilo(double x, const LogTab &lt, do
     p = __builtin_fma(p, r, c.l5);            // 1/5
     p = __builtin_fma(p, r, c.l4);            // -1/4
     p = __builtin_fma(p, r, c.l3);            // 1/3
+#if LDPC_L2_INLINE
+    p = __builtin_fma(p, r, -0.5);  // == c.l2; -0.5 is an inline f64 operand (no register)
+#else
     p = __builtin_fma(p, r, c.l2);            // -1/2
+#endif
     lo = ((w - hi) + r) + (__builtin_fma(kd, c.ln2lo, t.lo) + r2 * p);
 }
 

@@ -262,7 +262,11 @@ __device__ __forceinline__ bool tile_t(const TileCtx &c, double &t, double eo) {
     if (LDPC_TILE_TANH_BF) {
         const double d = M * 0.5;
         const double r = np_tanh(d, c.ttab);
+#if LDPC_CLIP_ABS
+        t = __builtin_fabs(d) > 17.5 ? __builtin_copysign(kCL, d) : r;  // :138-146 (cn_tanh, as selects)
+#else
         t = d > 17.5 ? kCL : (d < -17.5 ? -kCL : r);  // :138-146 (cn_tanh, as selects)
+#endif
     } else {
         t = cn_tanh(M, c.ttab);
     }
