@@ -1,21 +1,25 @@
 #!/usr/bin/env python3
 """Headline benchmark: decoded codewords/s (+ info-bits/s) of the on-device
-Monte-Carlo step on MI355X, BASELINE.json configs[1]:
+Monte-Carlo step on MI355X, BASELINE.json configs[2] (the north-star code):
 
-    WiMAX n=576 rate-1/2 (wimax_576_0.5), SPA fp64, max 50 iterations with the
-    reference's early-termination syndrome, 65,536 frames per GPU per step,
-    reference SNR axis 0 dB (speed 1.0).
+    WiMAX n=2304 rate-1/2 (wimax_2304_0.5), SPA fp64, max 50 iterations with
+    the reference's early-termination syndrome, reference SNR axis 1.0 dB
+    (speed 1.0).  The config's 262,144-frame batch is run as 32,768-frame
+    steps with the global frame index continuing (8 steps cover the batch).
 
-A step = one pass of the hot path over one batch: generate 65,536 synthetic
+A step = one pass of the hot path over one batch: generate 32,768 synthetic
 frames on the GPU (info bits -> [u, A.u] -> BPSK -> AWGN -> LLR), decode them
-(CN + VN/syndrome kernels, up to 50 iterations) and reduce the five
-main.py counters on the device.  With N GPUs (one process per GPU, launched by
+(up to 50 iterations with early termination) and reduce the main.py counters
+on the device.  With N GPUs (one process per GPU, launched by
 torch.distributed.run) every rank decodes its own disjoint frame range and the
-counters are summed with ONE all-reduce over RCCL (weak scaling).
+counters are summed with ONE all-reduce (weak scaling).  After the timed
+region, one step each at --extra-snr points (default 2.0 and 3.0 dB) is timed
+and reported under "snr_points".
 
 Output: ONE JSON line on rank 0 (contract in the task statement), with
-`roofline` for the dominant kernel (cn_kernel, timed live with HIP events on
-its own stream) and `cpu_baseline` (the C oracle, OpenMP, bounded sample).
+`roofline` for the whole decode (algorithmic bytes, SURVEY.md section 8d, over
+the decode kernels' HIP-event time on the decoder's stream) and `cpu_baseline`
+(the C oracle, OpenMP over all usable host cores, bounded sample).
 """
 import argparse
 import json
@@ -39,11 +43,13 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--code", default="wimax_576_0.5")
-    ap.add_argument("--frames", type=int, default=65536, help="frames per GPU per step")
+    ap.add_argument("--code", default="wimax_2304_0.5")
+    ap.add_argument("--frames", type=int, default=32768, help="frames per GPU per step")
     ap.add_argument("--chunk", type=int, default=0,
                     help="decoder slots (frames resident at once); 0 = whole batch, capped by an HBM budget "
-                         "(Decoder.fit_slots, LDPC_HBM_BUDGET_GB, default 160)")
+                         "(Decoder.fit_slots, --hbm-budget-gb)")
+    ap.add_argument("--hbm-budget-gb", type=float, default=220.0,
+                    help="HBM the decoder workspace may take (of 288 GB per MI355X)")
     ap.add_argument("--schedule", choices=("auto", "stream", "static"), default="auto",
                     help="stream: a slot takes the next frame as soon as its frame stops; static: chunks decoded "
                          "to completion (same frames, same counters); auto: static where the tile-resident "
@@ -51,9 +57,11 @@ def parse():
     ap.add_argument("--split", action="store_true",
                     help="parity mode: per-iteration CN/VN launches even where the tile-resident decoder applies")
     ap.add_argument("--iters", type=int, default=50)
-    ap.add_argument("--snr", type=float, default=0.0, help="reference SNR axis (dB), speed=1")
+    ap.add_argument("--snr", type=float, default=1.0, help="reference SNR axis (dB), speed=1")
+    ap.add_argument("--extra-snr", default="2.0,3.0",
+                    help="comma-separated SNR points timed for one step each after the headline ('' = none)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU-baseline sample budget (0 = skip)")
-    ap.add_argument("--cpu-threads", type=int, default=0)
+    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = every usable host core (usable_cores())")
     ap.add_argument("--mode", choices=("parity", "physical"), default="parity",
                     help="parity: the reference's fp64 decoder on H_std (headline); physical: "
                          "SURVEY §8 f4, standard SPA on the sparse graph, fp32, LDS-resident")
@@ -136,13 +144,38 @@ def committed_traffic(nnz, frames, kernel="cn"):
     return best or (None, None)
 
 
+def usable_cores():
+    """Host cores this process may run on: the affinity mask, capped by the
+    cgroup CPU quota when one is set (a GPU box's share of a larger machine:
+    os.cpu_count() there counts the whole machine).  -> (cores, affinity, quota)."""
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except AttributeError:
+        aff = os.cpu_count() or 1
+    quota = None
+    for path in ("/sys/fs/cgroup/cpu.max", "/sys/fs/cgroup/cpu/cpu.cfs_quota_us"):
+        try:
+            parts = open(path).read().split()
+        except OSError:
+            continue
+        if path.endswith("cpu.max") and parts and parts[0] != "max":
+            quota = int(parts[0]) / int(parts[1])
+        elif path.endswith("quota_us") and parts and int(parts[0]) > 0:
+            period = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+            quota = int(parts[0]) / period
+        break
+    cores = aff if quota is None else max(1, min(aff, int(math.ceil(quota))))
+    return cores, aff, quota
+
+
 def cpu_baseline(H, k, args):
     """The C oracle (oracle/spa_oracle.c, OpenMP over frames) on a bounded
     sample of the same workload; frames from the oracle's restatement of the
-    device frame source."""
+    device frame source.  Every usable host core (usable_cores())."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle
-    threads = args.cpu_threads or min(16, os.cpu_count() or 1)
+    cores, aff, quota = usable_cores()
+    threads = args.cpu_threads or cores
     sigma = oracle.sigma_for_snr(args.snr)
     per = max(2 * threads, 16)
     done, iters, t0 = 0, 0, time.perf_counter()
@@ -158,7 +191,11 @@ def cpu_baseline(H, k, args):
     dt = time.perf_counter() - t0
     return {"value": done / dt, "unit": "codewords/s", "cores": threads, "kind": "port",
             "sample": f"{done} frames of {args.code}, T={args.iters}, snr={args.snr} dB "
-                      f"({iters} frame-iterations) in {dt:.1f} s; oracle/spa_oracle.c -O2 OpenMP",
+                      f"({iters} frame-iterations) in {dt:.1f} s; oracle/spa_oracle.c -O2 OpenMP, "
+                      f"{threads} threads",
+            "host_cpus_affinity": aff, "cgroup_cpu_quota": quota,
+            "calibration": "profiles/r2_cpu_calibration/calibration.json (oracle vs the reference main.py, "
+                           "same config and cores, build container)",
             "info_bits_per_s": done * k / dt}
 
 
@@ -168,7 +205,7 @@ def cpu_baseline_phys(H, k, args, ira_code):
     from concurrent.futures import ThreadPoolExecutor
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle
-    threads = args.cpu_threads or min(16, os.cpu_count() or 1)
+    threads = args.cpu_threads or usable_cores()[0]
     sigma = oracle.sigma_for_snr(args.snr)
     Hp, Hgen = H
 
@@ -220,7 +257,8 @@ def main():
         graph = Graph(H, device=local)
         Hphys = edd.physical_matrix() if args.mode == "physical" else None
         pgraph = Graph(Hphys, device=local) if Hphys is not None else None
-    chunk = args.chunk or Decoder.fit_slots(graph, args.frames)  # whole batch, if its state fits the HBM budget
+    # whole batch resident, if its state fits the HBM budget
+    chunk = args.chunk or Decoder.fit_slots(graph, args.frames, budget=args.hbm_budget_gb * 1e9)
     dec = Decoder(graph, chunk)
     if args.schedule == "auto":
         from ldpc_amd import _lib
@@ -231,12 +269,13 @@ def main():
 
     local_totals = np.zeros((1, 7), np.int64)
 
-    def step(s, record=False):
+    def step(s, record=False, sig=None):
+        sig = sigma if sig is None else sig
         frame0 = (s * world + rank) * B  # disjoint global frame ranges per rank and step
         if pgraph is not None:
-            c = dec.phys_mc_run(pgraph, SEED, [sigma], B, frame0, args.iters, hbm=args.phys_hbm)
+            c = dec.phys_mc_run(pgraph, SEED, [sig], B, frame0, args.iters, hbm=args.phys_hbm)
         else:
-            c = dec.mc_run(SEED, [sigma], B, frame0, args.iters, static=args.schedule == "static", split=args.split)
+            c = dec.mc_run(SEED, [sig], B, frame0, args.iters, static=args.schedule == "static", split=args.split)
         if record:
             local_totals[:] += c
         return allreduce_counters(dist, c, local)
@@ -256,6 +295,21 @@ def main():
     dec.profile(False)
     prof = dec.profile_read()
     elapsed = max_over_ranks(dist, elapsed, local)
+
+    # extra SNR points (one step each, after the headline's timed region)
+    snr_points = []
+    for i, x in enumerate(v for v in args.extra_snr.split(",") if v.strip()):
+        x = float(x)
+        sg = 1.0 / math.sqrt(2.0 * 1.0 * (10.0 ** (x * 0.1)))
+        barrier(dist, local)
+        t1 = time.perf_counter()
+        c = step(args.warmup + args.steps + i, sig=sg)
+        barrier(dist, local)
+        dt = max_over_ranks(dist, time.perf_counter() - t1, local)
+        f = int(c[0, 0])
+        snr_points.append({"snr_db": x, "value": f / dt, "unit": "codewords/s", "info_bits_per_s": f * k / dt,
+                           "ms": dt * 1e3, "frames": f, "avg_iters": int(c[0, 6]) / max(f, 1),
+                           "fer": int(c[0, 1]) / max(f, 1), "ber": int(c[0, 2]) / (k * max(f, 1))})
 
     frames_total = int(totals[0, 0])
     assert frames_total == B * world * args.steps, (frames_total, B, world, args.steps)
@@ -324,6 +378,28 @@ def main():
                             "count_ms": prof["count"][0]},
         "cpu_baseline": None,
     }
+    if snr_points:
+        out["snr_points"] = snr_points
+    if not tile_launches and pgraph is None and cn_launches:
+        # separate CN / VN launches: the roofline is the WHOLE decode, one "launch" = one
+        # CN + one VN sweep over the resident slots; traffic = PMC bytes of the same pair
+        out["cn_roofline"] = out["roofline"]
+        tc, src_c = committed_traffic(nnz, chunk, "cn")
+        tv, src_v = committed_traffic(nnz, chunk, "vn")
+        read_bytes = frames_local * 8 * n + 8.0 * nnz * local_iters
+        out["roofline"] = {
+            "bound": "hbm", "achieved": decode_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": decode_gbs / HBM_PEAK_GBS,
+            "traffic": (tc + tv) if (tc is not None and tv is not None) else None,
+            "traffic_source": src_c if src_c == src_v else None,
+            "kernel": f"{cn_name}+vn_kernel", "launches": cn_launches,
+            "avg_launch_ms": decode_ms / cn_launches, "bytes_per_launch": dec_bytes / cn_launches,
+            "bytes_model": "per frame 8 n (channel LLRs) + 16 B x H_std edges x iterations executed "
+                           "(E_old read + E_new write) + ceil(n/8) + 8 (SURVEY 8d), over the CN + VN "
+                           "launches' HIP-event time",
+            "read_achieved": read_bytes / (decode_ms / 1e3) / 1e9,
+            "read_frac": read_bytes / (decode_ms / 1e3) / 1e9 / HBM_PEAK_GBS,
+        }
     if tile_launches and pgraph is None:
         # the whole decode is one kernel: algorithmic bytes per decoded frame
         # 8n + sum_iters 16 E + ceil(n/8) + 8, over this rank's frames, per launch

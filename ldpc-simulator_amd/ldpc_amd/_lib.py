@@ -3,6 +3,15 @@
 The shared library is built in-tree (``ldpc-simulator_amd/csrc/Makefile`` ->
 ``ldpc_amd/libldpc_hip.so``).  There is no fallback: if the library is
 missing, or a compute entry point is called without a GPU, this module raises.
+
+Fork safety (main.py:221 builds an SPA_Decoder in the parent, then
+main.py:248-256 forks a ProcessPoolExecutor whose workers build their own,
+main.py:78; adaptive.py:227-282 likewise).  Loading the library does not start
+the HIP runtime; the first call through ``gpu()`` does, and records the pid.
+A process forked from a parent that had started HIP cannot use the inherited
+runtime, so ``gpu()`` in such a child raises LdpcError instead of touching
+it; a child of a parent that never did (the main.py pattern: construction is
+HIP-free, see spa_decoder.py) starts its own.
 """
 import ctypes
 import os
@@ -43,6 +52,8 @@ class LdpcError(RuntimeError):
 
 _lock = threading.Lock()
 _lib = None
+_gpu_pid = None  # pid of the process that started the HIP runtime through gpu()
+LDPC_EFORK = -100  # Python-side code: HIP was started in a parent process before fork
 
 P = ctypes.POINTER
 c_i32, c_i64, c_u32, c_u64, c_dbl, c_vp = (ctypes.c_int32, ctypes.c_int64, ctypes.c_uint32,
@@ -105,9 +116,31 @@ def lib():
     return _lib
 
 
+def gpu():
+    """The library handle for calls that use the HIP runtime (every entry point
+    except ldpc_hstd_*, ldpc_last_error, ldpc_abi_version).  Raises in a
+    process forked after its parent started HIP (see the module docstring)."""
+    global _gpu_pid
+    pid = os.getpid()
+    if _gpu_pid is not None and _gpu_pid != pid:
+        raise LdpcError("gpu", LDPC_EFORK,
+                        f"the HIP runtime was started in process {_gpu_pid} before it forked this process "
+                        f"({pid}); a forked child cannot use it.  Construct SPA_Decoder objects freely in the "
+                        "parent (construction does not start HIP) but decode only in the workers, or use the "
+                        "'spawn' start method")
+    h = lib()
+    _gpu_pid = pid
+    return h
+
+
+def hip_started_here():
+    """Whether this process has started the HIP runtime through gpu()."""
+    return _gpu_pid == os.getpid()
+
+
 def check(fn_name, rc):
     if rc != 0:
-        msg = lib().ldpc_last_error()
+        msg = lib().ldpc_last_error()  # thread-local string, no HIP
         raise LdpcError(fn_name, rc, msg.decode() if msg else "")
     return rc
 
@@ -125,7 +158,7 @@ def i32p(a):
 
 
 def device_count():
-    return int(lib().ldpc_device_count())
+    return int(gpu().ldpc_device_count())
 
 
 def as_i32(a):

@@ -1,9 +1,13 @@
 """Python handles over the C ABI: the graph on a GPU and a decoder workspace.
 
 ``Graph``   wraps ldpc_graph_create (H_std uploaded once per device, cached by
-            content so repeated SPA_Decoder constructions -- main.py:221 builds
-            one per SNR point, main.py:78 one per frame -- do not re-upload).
+            content and process so repeated SPA_Decoder constructions --
+            main.py:221 builds one per SNR point, main.py:78 one per frame --
+            do not re-upload, and a forked worker never gets its parent's
+            device handle).
 ``Decoder`` wraps ldpc_decoder_create / ldpc_decode_f64 / ldpc_mc_run.
+Every call here goes through _lib.gpu() (fork check, _lib's docstring); a
+handle is only released by the process that created it.
 """
 import ctypes
 import hashlib
@@ -37,11 +41,12 @@ class Graph:
         self.indptr, self.indices = indptr, indices
         self.nnz = int(indptr[-1])
         h = ctypes.c_void_p()
-        check("ldpc_graph_create", _lib.lib().ldpc_graph_create(
+        check("ldpc_graph_create", _lib.gpu().ldpc_graph_create(
             m, n, _lib.i32p(indptr), _lib.i32p(indices), int(device), ctypes.byref(h)))
         self._h = h
+        self._pid = os.getpid()
         mr, mc = ctypes.c_int32(), ctypes.c_int32()
-        check("ldpc_graph_info", _lib.lib().ldpc_graph_info(h, None, None, None, ctypes.byref(mr), ctypes.byref(mc)))
+        check("ldpc_graph_info", _lib.gpu().ldpc_graph_info(h, None, None, None, ctypes.byref(mr), ctypes.byref(mc)))
         self.max_row_deg, self.max_col_deg = mr.value, mc.value
 
     @property
@@ -51,7 +56,7 @@ class Graph:
     @classmethod
     def cached(cls, H, device=-1):
         m, n, indptr, indices = _csr_arrays(H)
-        key = (m, n, int(device), hashlib.sha1(indptr.tobytes() + indices.tobytes()).hexdigest())
+        key = (os.getpid(), m, n, int(device), hashlib.sha1(indptr.tobytes() + indices.tobytes()).hexdigest())
         with cls._cache_lock:
             g = cls._cache.get(key)
             if g is None:
@@ -61,9 +66,9 @@ class Graph:
 
     def __del__(self):
         h = getattr(self, "_h", None)
-        if h is not None and h.value and _lib._lib is not None:
+        if h is not None and h.value and _lib._lib is not None and getattr(self, "_pid", None) == os.getpid():
             _lib._lib.ldpc_graph_destroy(h)
-            self._h = None
+        self._h = None
 
 
 def phys_decode(graph, llr, max_iter, post=False, hbm=False):
@@ -79,7 +84,7 @@ def phys_decode(graph, llr, max_iter, post=False, hbm=False):
     status = np.empty(B, np.int32)
     iters = np.empty(B, np.int32)
     Lp = np.empty((B, n), np.float32) if post else None
-    check("ldpc_phys_decode", _lib.lib().ldpc_phys_decode(
+    check("ldpc_phys_decode", _lib.gpu().ldpc_phys_decode(
         graph.handle, B, _lib.ptr(llr), int(max_iter), LDPC_F_PHYS_HBM if hbm else 0, _lib.ptr(z), _lib.ptr(conv),
         _lib.ptr(status),
         _lib.ptr(iters), _lib.ptr(Lp), None))
@@ -96,13 +101,14 @@ class Decoder:
     def __init__(self, graph, max_frames=4096):
         self.graph = graph
         h = ctypes.c_void_p()
-        check("ldpc_decoder_create", _lib.lib().ldpc_decoder_create(graph.handle, int(max_frames), ctypes.byref(h)))
+        check("ldpc_decoder_create", _lib.gpu().ldpc_decoder_create(graph.handle, int(max_frames), ctypes.byref(h)))
         self._h = h
-        self.capacity = int(_lib.lib().ldpc_decoder_capacity(h))
+        self._pid = os.getpid()
+        self.capacity = int(_lib.gpu().ldpc_decoder_capacity(h))
 
     @staticmethod
     def workspace_bytes(graph, max_frames):
-        return int(_lib.lib().ldpc_decoder_bytes(graph.handle, int(max_frames)))
+        return int(_lib.gpu().ldpc_decoder_bytes(graph.handle, int(max_frames)))
 
     # HBM the Monte-Carlo drivers let one decoder take (of 288 GB per MI355X);
     # LDPC_HBM_BUDGET_GB overrides
@@ -146,7 +152,7 @@ class Decoder:
         hi = np.empty((B, T), np.float64) if (hist and nllr) else None
         E = np.empty((B, g.nnz), np.float64) if msgs else None
         flags = (LDPC_F_NLLR if nllr else 0) | (LDPC_F_SPLIT if split else 0)
-        check("ldpc_decode_f64", _lib.lib().ldpc_decode_f64(
+        check("ldpc_decode_f64", _lib.gpu().ldpc_decode_f64(
             self._h, B, _lib.ptr(llr), T, flags, _lib.ptr(z), _lib.ptr(conv), _lib.ptr(status),
             _lib.ptr(Lp), _lib.ptr(nl), _lib.ptr(hi), _lib.ptr(iters), _lib.ptr(E), None))
         return DecodeResult(z=z, conv=conv, status=status, iters=iters, nllr=nl, post=Lp, hist=hi, msgs=E)
@@ -166,7 +172,7 @@ class Decoder:
             raise ValueError(f"llr must be [batch, {self.graph.n}]")
         flags = LDPC_F_DEVICE_PTRS | (LDPC_F_NLLR if (nllr is not None or hist is not None) else 0) | \
             (LDPC_F_SPLIT if split else 0)
-        check("ldpc_decode_f64", _lib.lib().ldpc_decode_f64(
+        check("ldpc_decode_f64", _lib.gpu().ldpc_decode_f64(
             self._h, B, dp(llr), int(max_iter), flags, dp(z), dp(conv), dp(status), dp(post), dp(nllr), dp(hist),
             dp(iters), None, ctypes.c_void_p(int(stream)) if stream else None))
 
@@ -175,7 +181,7 @@ class Decoder:
         g = self.graph
         u = np.empty((count, g.k), np.uint8)
         llr = np.empty((count, g.n), np.float64)
-        check("ldpc_generate_frames", _lib.lib().ldpc_generate_frames(
+        check("ldpc_generate_frames", _lib.gpu().ldpc_generate_frames(
             self._h, int(seed), int(snr_point), float(sigma), int(frame0), int(count), 0,
             _lib.ptr(u), _lib.ptr(llr), None))
         return u, llr
@@ -189,7 +195,7 @@ class Decoder:
         sig = np.ascontiguousarray(np.asarray(sigmas, dtype=np.float64))
         out = np.zeros((len(sig), LDPC_MC_NCOUNT), np.int64)
         flags = (LDPC_F_NLLR if nllr else 0) | (LDPC_F_STATIC if static else 0) | (LDPC_F_SPLIT if split else 0)
-        check("ldpc_mc_run", _lib.lib().ldpc_mc_run(
+        check("ldpc_mc_run", _lib.gpu().ldpc_mc_run(
             self._h, int(seed), len(sig), sig.ctypes.data_as(ctypes.POINTER(ctypes.c_double)),
             int(frames_per_point), int(frame0), int(max_iter), flags,
             out.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)), None))
@@ -202,7 +208,7 @@ class Decoder:
         code, phys_graph itself.  hbm=True forces the HBM-resident tile path."""
         sig = np.ascontiguousarray(np.asarray(sigmas, dtype=np.float64))
         out = np.zeros((len(sig), LDPC_MC_NCOUNT), np.int64)
-        check("ldpc_phys_mc_run", _lib.lib().ldpc_phys_mc_run(
+        check("ldpc_phys_mc_run", _lib.gpu().ldpc_phys_mc_run(
             self._h, phys_graph.handle, int(seed), len(sig), sig.ctypes.data_as(ctypes.POINTER(ctypes.c_double)),
             int(frames_per_point), int(frame0), int(max_iter), LDPC_F_PHYS_HBM if hbm else 0,
             out.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)), None))
@@ -211,18 +217,18 @@ class Decoder:
     KINDS = ("cn", "vn", "generate", "count", "phys", "phys_cn", "phys_vn", "tile")
 
     def profile(self, enable=True):
-        check("ldpc_profile_enable", _lib.lib().ldpc_profile_enable(self._h, 1 if enable else 0))
+        check("ldpc_profile_enable", _lib.gpu().ldpc_profile_enable(self._h, 1 if enable else 0))
 
     def profile_read(self):
         """{kind: (total_ms, launches)} of this decoder's launches since the last read."""
         ms = (ctypes.c_double * len(self.KINDS))()
         n = (ctypes.c_int64 * len(self.KINDS))()
-        check("ldpc_profile_read", _lib.lib().ldpc_profile_read(self._h, ms, n))
+        check("ldpc_profile_read", _lib.gpu().ldpc_profile_read(self._h, ms, n))
         return {k: (ms[i], n[i]) for i, k in enumerate(self.KINDS)}
 
     def close(self):
         h = getattr(self, "_h", None)
-        if h is not None and h.value and _lib._lib is not None:
+        if h is not None and h.value and _lib._lib is not None and getattr(self, "_pid", None) == os.getpid():
             _lib._lib.ldpc_decoder_destroy(h)
         self._h = None
 

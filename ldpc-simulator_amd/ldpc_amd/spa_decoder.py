@@ -3,7 +3,13 @@
 Same constructor and call as python_ldpc_app/spa_decoder.py:
     SPA_Decoder(encoder_decoder_data, settings)            (:16-42)
     decode(data_buffer) -> Result                          (:63-280)
-reads data_buffer._channel_data, writes data_buffer._decoded_data (the hard
+Construction does no HIP work: the graph upload and the device workspace are
+made by the first decode() in the process that calls it.  main.py:221 builds
+a decoder in the parent and then forks a ProcessPoolExecutor whose workers
+build their own (main.py:78, main.py:248-256; adaptive.py:227-282): the
+parent never starts HIP, each worker starts its own (ldpc_amd._lib.gpu).
+
+decode() reads data_buffer._channel_data, writes data_buffer._decoded_data (the hard
 output z, the complement of the bit estimate), and sets convergence_iteration,
 _normalized_llr_by_iterations (appended per iteration, never reset -- :19-22,
 :226-228) and _d_summarize_normalized_llr.  Failure to converge is
@@ -13,6 +19,8 @@ Result.DATA_TRANSFER_NOT_OK, not an exception; bad arguments raise.
 reference's: only `_h_sparse_cached` (else `_h_std`), `_m` and `_n` are read,
 as the reference does.  `decode_batch` decodes many frames per launch.
 """
+import os
+
 import numpy as np
 from scipy import sparse
 
@@ -43,16 +51,27 @@ class SPA_Decoder:
             raise ValueError(f"H_std shape {H.shape} != (m, n) = "
                              f"({encoder_decoder_data._m}, {encoder_decoder_data._n})")
         self.H_sparse = H
-        self._graph = Graph.cached(H, device)
-        self._dev = Decoder(self._graph, max_frames)
+        self._device_index = device
+        self._max_frames = max_frames
+        self._graph = None
+        self._dev = None
+        self._pid = None
         self._Result = caller_result_enum()
+
+    def _device(self):
+        """Graph + workspace of THIS process, made on first use (no HIP in __init__)."""
+        if self._dev is None or self._pid != os.getpid():
+            self._graph = Graph.cached(self.H_sparse, self._device_index)
+            self._dev = Decoder(self._graph, self._max_frames)
+            self._pid = os.getpid()
+        return self._dev
 
     # ------------------------------------------------------------ one frame
     def decode(self, p_data_buffer):
         T = int(self.m_pSettings.get_max_iterations())
         nllr = bool(self.m_pSettings.is_normalized_llr_calculate())
         ch = np.asarray(p_data_buffer._channel_data, dtype=np.float64)
-        r = self._dev.decode(ch[None, :], T, nllr=nllr, hist=nllr)
+        r = self._device().decode(ch[None, :], T, nllr=nllr, hist=nllr)
         self.convergence_iteration = int(r.conv[0])
         p_data_buffer._decoded_data = r.z[0].astype(np.int64).tolist()
         if nllr:
@@ -73,8 +92,10 @@ class SPA_Decoder:
         nl = bool(self.m_pSettings.is_normalized_llr_calculate() if nllr is None else nllr)
         llr = np.asarray(llr, dtype=np.float64)
         B = llr.shape[0] if llr.ndim == 2 else 1
-        dev = self._dev
-        want = max_frames or B
+        dev = self._device()
+        # a workspace for the whole batch if it fits the HBM budget, else
+        # ldpc_decode_f64 runs the batch in chunks of the capacity
+        want = max_frames or Decoder.fit_slots(self._graph, B)
         if want > dev.capacity:
             dev = self._dev = Decoder(self._graph, want)
         return dev.decode(llr, T, nllr=nl, post=post, hist=hist, msgs=msgs)

@@ -240,11 +240,11 @@ def main():
         need.add("BCH_7_4_1_strip")
     if want("codes") or any(want(s) for s in ("w576_T5", "w576_T50", "w576_edge")):
         need.add("wimax_576_0.5")
-    if want("codes") or want("w2304_T3"):
+    if want("codes") or any(want(s) for s in ("w2304_T3", "w2304_T10", "w2304_T50")):
         need.add("wimax_2304_0.5")
-    if want("codes") or want("w2304A_T2"):
+    if want("codes") or any(want(s) for s in ("w2304A_T2", "w2304A_T3_4dB")):
         need.add("wimax_2304_0.75A")
-    if want("codes"):
+    if want("codes") or want("w2304B_T2"):
         need.add("wimax_2304_0.75B")
     for name in CODES:
         if name in need:
@@ -269,6 +269,15 @@ def main():
             run_set(pool, "w2304_T3", "wimax_2304_0.5", 3, [0.0, 3.0], 2, True, 7000)
         if want("w2304A_T2"):
             run_set(pool, "w2304A_T2", "wimax_2304_0.75A", 2, [2.0], 2, False, 8000)
+        # round 2: depth on the north-star code and the r3/4 variants
+        if want("w2304_T10"):
+            run_set(pool, "w2304_T10", "wimax_2304_0.5", 10, [1.0, 2.0, 3.0], 4, True, 9000)
+        if want("w2304_T50"):
+            run_set(pool, "w2304_T50", "wimax_2304_0.5", 50, [1.0, 3.0], 2, False, 9500)
+        if want("w2304A_T3_4dB"):  # the r3/4A FER-1.0 cliff, in the reference itself
+            run_set(pool, "w2304A_T3_4dB", "wimax_2304_0.75A", 3, [4.0], 4, False, 10000)
+        if want("w2304B_T2"):
+            run_set(pool, "w2304B_T2", "wimax_2304_0.75B", 2, [2.0], 2, False, 11000)
 
 
 if __name__ == "__main__":

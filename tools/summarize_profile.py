@@ -46,7 +46,12 @@ def main(src, dst, nnz, frames):
     vn_alg = 8.0 * nnz * frames  # each message read once (+ ch: n/nnz ~ 1.4 % on 576)
     factor = vn_alg / (agg[vn]["FETCH_SIZE"] * 1024.0)
     out = {"fetch_correction_factor": factor, "frames": frames, "edges": nnz, "kernels": {}}
-    for role, k in (("cn", cn), ("vn", vn)):
+    roles = [("cn", cn), ("vn", vn)]
+    try:
+        roles.append(("refill", busiest(("refill_kernel",), agg)))
+    except KeyError:
+        pass
+    for role, k in roles:
         rd = agg[k]["FETCH_SIZE"] * 1024.0 * factor
         wr = agg[k]["WRITE_SIZE"] * 1024.0
         s = stats[k] if k in stats else next(v for n, v in stats.items() if n.startswith(k[:40]))
