@@ -67,10 +67,67 @@ def parse():
                          "SURVEY §8 f4, standard SPA on the sparse graph, fp32, LDS-resident")
     ap.add_argument("--phys-hbm", action="store_true",
                     help="physical mode: HBM-resident state even when a frame fits in LDS")
+    ap.add_argument("--comm", choices=("rccl", "torch"), default="rccl",
+                    help="N>1 exchange: rccl = RCCL through the C ABI (ldpc_amd.comm, no PyTorch); "
+                         "torch = torch.distributed with --dist-backend")
     ap.add_argument("--dist-backend", default="nccl",
-                    help="torch.distributed backend for N>1 ('nccl' = RCCL over xGMI; 'gloo' for "
-                         "rehearsing several ranks on one GPU)")
+                    help="--comm torch only: 'nccl' (= RCCL) or 'gloo' (rehearse several ranks on one GPU)")
     return ap.parse_args()
+
+
+class RcclDist:
+    """The N>1 exchange through the C ABI (ldpc_amd.comm: RCCL over xGMI, file
+    rendezvous of the unique id, no PyTorch)."""
+
+    def __init__(self, device):
+        from ldpc_amd.comm import Comm
+        self.c = Comm.from_env(device)
+        self.device = device
+
+    def allreduce(self, ctr):
+        return self.c.allreduce(np.asarray(ctr, np.int64))
+
+    def max(self, x):
+        return float(self.c.allreduce(np.array([x], np.float64), op="max")[0])
+
+    def barrier(self):
+        self.c.barrier()  # all ranks arrive, then hipDeviceSynchronize
+
+    def close(self):
+        self.c.close()
+
+
+class TorchDist:
+    """--comm torch: the same exchange through torch.distributed (backend 'nccl'
+    = RCCL, or 'gloo' to rehearse several ranks on one GPU)."""
+
+    def __init__(self, device, backend):
+        import torch
+        import torch.distributed as dist
+        torch.cuda.set_device(device)
+        if backend == "nccl":  # bind the rank's GPU explicitly
+            dist.init_process_group("nccl", device_id=torch.device(f"cuda:{device}"))
+        else:
+            dist.init_process_group(backend)
+        self.torch, self.dist, self.device = torch, dist, device
+        self.dev = "cpu" if backend == "gloo" else f"cuda:{device}"
+
+    def allreduce(self, ctr):
+        t = self.torch.from_numpy(np.asarray(ctr, np.int64).reshape(-1).copy()).to(self.dev)
+        self.dist.all_reduce(t)
+        return t.cpu().numpy().reshape(np.shape(ctr))
+
+    def max(self, x):
+        t = self.torch.tensor([x], dtype=self.torch.float64, device=self.dev)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
+        return float(t.item())
+
+    def barrier(self):
+        self.dist.barrier()
+        self.torch.cuda.synchronize(self.device)
+
+    def close(self):
+        self.dist.destroy_process_group()
 
 
 def dist_setup(args):
@@ -78,51 +135,26 @@ def dist_setup(args):
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
-    device = local
-    # LDPC_BENCH_FORCE_DIST=1: the N>1 code path (torch first, RCCL process
-    # group, counter all-reduce, max over ranks) with a single rank -- how the
+    # LDPC_BENCH_FORCE_DIST=1: the N>1 code path (communicator, counter
+    # all-reduce, barriers, max over ranks) with a single rank -- how the
     # driver's multi-GPU run is rehearsed on a one-GPU box
     if world > 1 or os.environ.get("LDPC_BENCH_FORCE_DIST") == "1":
-        import torch
-        import torch.distributed as dist
-        device = local % max(1, torch.cuda.device_count())
-        torch.cuda.set_device(device)
-        if args.dist_backend == "nccl":  # RCCL on ROCm; bind the rank's GPU explicitly
-            dist.init_process_group("nccl", device_id=torch.device(f"cuda:{device}"))
-        else:
-            dist.init_process_group(args.dist_backend)
-    return world, rank, device, dist
-
-
-def _dev(dist, local):
-    return "cpu" if dist.get_backend() == "gloo" else f"cuda:{local}"
+        dist = RcclDist(local) if args.comm == "rccl" else TorchDist(local, args.dist_backend)
+    return world, rank, local, dist
 
 
 def allreduce_counters(dist, ctr, local):
-    """The single RCCL all-reduce of the error counters (int64 vector)."""
-    if dist is None:
-        return ctr
-    import torch
-    t = torch.from_numpy(ctr.reshape(-1).copy()).to(_dev(dist, local))
-    dist.all_reduce(t)
-    return t.cpu().numpy().reshape(ctr.shape)
+    """The single all-reduce of the error counters (int64 [points x 7])."""
+    return ctr if dist is None else dist.allreduce(ctr)
 
 
 def barrier(dist, local):
     if dist is not None:
-        import torch
         dist.barrier()
-        if torch.cuda.is_available():
-            torch.cuda.synchronize(local)
 
 
 def max_over_ranks(dist, x, local):
-    if dist is None:
-        return x
-    import torch
-    t = torch.tensor([x], dtype=torch.float64, device=_dev(dist, local))
-    dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    return float(t.item())
+    return x if dist is None else dist.max(x)
 
 
 def committed_traffic(nnz, frames, kernel="cn"):
@@ -461,7 +493,7 @@ def main():
     if rank == 0:
         print(json.dumps(out), flush=True)
     if dist is not None:
-        dist.destroy_process_group()
+        dist.close()
 
 
 if __name__ == "__main__":

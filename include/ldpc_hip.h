@@ -220,6 +220,36 @@ int ldpc_profile_read(ldpc_decoder *d, double *ms_out, int64_t *launches_out);
  * uint64; returns the count written, or -1 in normal builds. */
 int ldpc_diag_tile_trace(uint64_t *out, int64_t n);
 
+/* ------------------------------------------------ multi-GPU (RCCL, xGMI)
+ * One process per GPU; frames are sharded by global index, so the only
+ * exchange is ONE all-reduce of the int64 counter matrix per Monte-Carlo step
+ * -- the reference's additive parent reduction of its workers' per-block
+ * results (main.py:149-175).  librccl.so.1 (ROCm) is loaded on first use with
+ * dlopen, so single-GPU users never load it.  No PyTorch.
+ *   1. rank 0: ldpc_comm_unique_id(id); hand the 128 bytes to every rank
+ *      (bench.py / ldpc_amd.comm: a file rendezvous on one node);
+ *   2. every rank: ldpc_comm_init(id, rank, world, device, &c);
+ *   3. ldpc_comm_allreduce(c, buf, count, dtype, op, flags, stream): in place;
+ *      host buffers unless LDPC_F_DEVICE_PTRS (then async on `stream`);
+ *      host buffers: synchronous.  dtype LDPC_DT_*, op LDPC_OP_*;
+ *   4. ldpc_comm_barrier(c): all ranks arrive, then the device is synchronised;
+ *   5. ldpc_comm_destroy(c).
+ */
+#define LDPC_COMM_ID_BYTES 128
+#define LDPC_DT_I64 0
+#define LDPC_DT_F64 1
+#define LDPC_OP_SUM 0
+#define LDPC_OP_MAX 1
+typedef struct ldpc_comm ldpc_comm;
+int ldpc_comm_unique_id(uint8_t *id_out);
+int ldpc_comm_init(const uint8_t *id, int32_t rank, int32_t world, int32_t device, ldpc_comm **out);
+int ldpc_comm_allreduce(ldpc_comm *c, void *buf, int64_t count, int32_t dtype, int32_t op, uint32_t flags,
+                        void *stream);
+int ldpc_comm_barrier(ldpc_comm *c);
+int ldpc_comm_destroy(ldpc_comm *c);
+/* hipDeviceSynchronize on `device` (bench.py's barrier brackets; no PyTorch) */
+int ldpc_device_synchronize(int32_t device);
+
 #ifdef __cplusplus
 }
 #endif

@@ -39,6 +39,8 @@ EXPORTED = (
     "ldpc_decode_f64", "ldpc_generate_frames", "ldpc_mc_run",
     "ldpc_profile_enable", "ldpc_profile_read", "ldpc_diag_tile_trace",
     "ldpc_phys_lds_bytes", "ldpc_phys_decode", "ldpc_phys_mc_run",
+    "ldpc_comm_unique_id", "ldpc_comm_init", "ldpc_comm_allreduce", "ldpc_comm_barrier", "ldpc_comm_destroy",
+    "ldpc_device_synchronize",
 )
 
 
@@ -93,6 +95,12 @@ def _declare(lib):
                                             P(c_i64), c_vp]),
         "ldpc_profile_read": (ctypes.c_int, [c_vp, P(c_dbl), P(c_i64)]),
         "ldpc_diag_tile_trace": (ctypes.c_int, [c_vp, c_i64]),
+        "ldpc_comm_unique_id": (ctypes.c_int, [c_vp]),
+        "ldpc_comm_init": (ctypes.c_int, [c_vp, c_i32, c_i32, c_i32, P(c_vp)]),
+        "ldpc_comm_allreduce": (ctypes.c_int, [c_vp, c_vp, c_i64, c_i32, c_i32, c_u32, c_vp]),
+        "ldpc_comm_barrier": (ctypes.c_int, [c_vp]),
+        "ldpc_comm_destroy": (ctypes.c_int, [c_vp]),
+        "ldpc_device_synchronize": (ctypes.c_int, [c_i32]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)

@@ -12,8 +12,9 @@ Reproduces the counter semantics of python_ldpc_app/main.py:run_simulation
 Multi-GPU (one process per GPU): rank r decodes the global frame indices
 [r*B/W, (r+1)*B/W) of every SNR point -- the Philox stream is keyed by the
 global index, so the counters are identical for any W -- and the whole
-[points x 7] counter matrix is summed with ONE all-reduce (RCCL over xGMI
-with backend "nccl"; gloo in CPU tests).
+[points x 7] counter matrix is summed with ONE all-reduce: RCCL over xGMI
+through the C ABI (ldpc_amd.comm, no PyTorch); CPU tests inject a gloo
+reducer (torch_allreduce) to exercise the same sharding logic.
 """
 import argparse
 import math
@@ -145,13 +146,11 @@ def main(argv=None):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    allreduce = None
+    allreduce = comm = None
     if world > 1:
-        import torch
-        import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl")
-        allreduce = torch_allreduce(f"cuda:{local}")
+        from .comm import Comm
+        comm = Comm.from_env(local)
+        allreduce = comm.allreduce
     snrs = snr_grid(a.initial_snr, a.end_snr, a.step_snr)
     res, _ = simulate(a.matrix, snrs, a.blocks, a.iterations, seed=a.seed, nllr=a.normalized_llr,
                       device=local, rank=rank, world=world, allreduce=allreduce)
@@ -163,9 +162,8 @@ def main(argv=None):
             res.to_json(a.output_json)
         if a.output_csv:
             res.to_csv(a.output_csv)
-    if world > 1:
-        import torch.distributed as dist
-        dist.destroy_process_group()
+    if comm is not None:
+        comm.close()
 
 
 if __name__ == "__main__":
