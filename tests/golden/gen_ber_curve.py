@@ -13,7 +13,12 @@ and records the per-point counters from its --output-json file
 the GPU Monte-Carlo sweep at the same points lies inside the binomial
 confidence interval of the reference's FER (and the BER ratio band).
 
-Usage:  python tests/golden/gen_ber_curve.py [--threads 6] [--points 1.0:96,1.5:128,...]
+Usage:  python tests/golden/gen_ber_curve.py [--code wimax_576_0.5] [--threads 6]
+                                            [--points 1.0:96,1.5:128,...]
+The north-star code (round 2): --code wimax_2304_0.5 --threads 4
+--points 3.0:64,1.0:8,2.0:16 (a 2304 frame-iteration costs ~25 s of one core
+in the reference, so the frame counts are small; the GPU test compares the
+reference's counts with the distribution of the GPU's at the same count).
 """
 import argparse
 import json
@@ -26,15 +31,13 @@ import time
 REF_APP = "/root/reference/python_ldpc_app"
 REF_DB = "/root/reference/Channel_Codes_Database"
 HERE = os.path.dirname(os.path.abspath(__file__))
-CODE = "wimax_576_0.5"
-ALIST = os.path.join(REF_DB, "Wimax LDPC Codes", CODE + ".alist.txt")
 T = 50
 DEFAULT_POINTS = "1.0:96,1.5:128,2.0:192,2.5:256,3.0:384"
 
 
-def run_point(snr, blocks, threads, tmp):
+def run_point(alist, snr, blocks, threads, tmp):
     out = os.path.join(tmp, f"snr_{snr}.json")
-    cmd = [sys.executable, os.path.join(REF_APP, "main.py"), "--matrix", ALIST, "--blocks", str(blocks),
+    cmd = [sys.executable, os.path.join(REF_APP, "main.py"), "--matrix", alist, "--blocks", str(blocks),
            "--iterations", str(T), "--decoder", "sumproduct", "--initial-snr", str(snr),
            "--end-snr", str(snr), "--step-snr", "0.5", "--ber", "--fer", "--threads", str(threads),
            "--output-json", out]
@@ -54,10 +57,14 @@ def run_point(snr, blocks, threads, tmp):
 
 def main():
     ap = argparse.ArgumentParser()
+    ap.add_argument("--code", default="wimax_576_0.5")
     ap.add_argument("--threads", type=int, default=6)
     ap.add_argument("--points", default=DEFAULT_POINTS)
-    ap.add_argument("--out", default=os.path.join(HERE, f"ber_curve_{CODE}.json"))
+    ap.add_argument("--out", default=None)
     a = ap.parse_args()
+    CODE = a.code
+    alist = os.path.join(REF_DB, "Wimax LDPC Codes", CODE + ".alist.txt")
+    a.out = a.out or os.path.join(HERE, f"ber_curve_{CODE}.json")
     points = [(float(s), int(b)) for s, b in (x.split(":") for x in a.points.split(","))]
     doc = {"code": CODE, "max_iter": T, "decoder": "sumproduct", "channel_mode": 1, "speed": 1.0,
            "source": "reference python_ldpc_app/main.py run in the build container (time-seeded RNG)",
@@ -69,7 +76,8 @@ def main():
         for snr, blocks in points:
             if snr in done:
                 continue
-            r = run_point(snr, blocks, a.threads, tmp)
+            r = run_point(alist, snr, blocks, a.threads, tmp)
+            r["threads"] = a.threads
             print(json.dumps(r), flush=True)
             doc["points"].append(r)
             doc["points"].sort(key=lambda p: p["snr_db"])
