@@ -301,13 +301,14 @@ def main():
 
     local_totals = np.zeros((1, 7), np.int64)
 
-    def step(s, record=False, sig=None):
+    def step(s, record=False, sig=None, schedule=None):
         sig = sigma if sig is None else sig
+        schedule = schedule or args.schedule
         frame0 = (s * world + rank) * B  # disjoint global frame ranges per rank and step
         if pgraph is not None:
             c = dec.phys_mc_run(pgraph, SEED, [sig], B, frame0, args.iters, hbm=args.phys_hbm)
         else:
-            c = dec.mc_run(SEED, [sig], B, frame0, args.iters, static=args.schedule == "static", split=args.split)
+            c = dec.mc_run(SEED, [sig], B, frame0, args.iters, static=schedule == "static", split=args.split)
         if record:
             local_totals[:] += c
         return allreduce_counters(dist, c, local)
@@ -328,19 +329,22 @@ def main():
     prof = dec.profile_read()
     elapsed = max_over_ranks(dist, elapsed, local)
 
-    # extra SNR points (one step each, after the headline's timed region)
+    # extra SNR points (one step each, after the headline's timed region), on
+    # the streaming schedule: there frames stop at very different iterations
     snr_points = []
+    extra_sched = "stream"
     for i, x in enumerate(v for v in args.extra_snr.split(",") if v.strip()):
         x = float(x)
         sg = 1.0 / math.sqrt(2.0 * 1.0 * (10.0 ** (x * 0.1)))
         barrier(dist, local)
         t1 = time.perf_counter()
-        c = step(args.warmup + args.steps + i, sig=sg)
+        c = step(args.warmup + args.steps + i, sig=sg, schedule=extra_sched)
         barrier(dist, local)
         dt = max_over_ranks(dist, time.perf_counter() - t1, local)
         f = int(c[0, 0])
         snr_points.append({"snr_db": x, "value": f / dt, "unit": "codewords/s", "info_bits_per_s": f * k / dt,
-                           "ms": dt * 1e3, "frames": f, "avg_iters": int(c[0, 6]) / max(f, 1),
+                           "ms": dt * 1e3, "frames": f, "schedule": extra_sched,
+                           "avg_iters": int(c[0, 6]) / max(f, 1),
                            "fer": int(c[0, 1]) / max(f, 1), "ber": int(c[0, 2]) / (k * max(f, 1))})
 
     frames_total = int(totals[0, 0])

@@ -940,24 +940,31 @@ size_t tile64_lds_bytes(const DevGraph &g) {
     return b <= kTileLdsMax ? b : 0;
 }
 
-// LDPC_TILE_SUB=1 (read at every decode) runs the long codes through the
-// sub-tile decoder; by default they take the separate CN/VN launches, which
-// measured faster (4.5k vs 4.2k cw/s on wimax_2304_0.5, 5.9k vs
-// 3.1k on wimax_2304_0.75A at 50 iterations).
-static bool sub_enabled() {
+// The sub-tile decoder (tile_sub.hip) for the long codes.  16-frame sub-tiles
+// (wimax_2304_0.5: the north-star code) are the default -- 0.337 vs 0.31 of
+// the HBM roofline for the separate CN/VN launches at 1 dB;
+// 8-frame sub-tiles (the r3/4 codes) measured slower than the separate
+// launches and stay opt-in.  LDPC_TILE_SUB (read at every decode): 0 = never,
+// 1 = also the 8-frame form, unset = the 16-frame form only.
+static int sub_mode() {
     const char *e = getenv("LDPC_TILE_SUB");
-    return e && atoi(e) == 1;
+    return e ? atoi(e) : -1;
+}
+static bool sub_enabled(const DevGraph &g) {
+    const int mode = sub_mode();
+    if (mode == 0) return false;
+    return mode == 1 || sub_frames(g) == 16;
 }
 
 size_t tile_lds_bytes(const DevGraph &g) {
     const size_t b = tile64_lds_bytes(g);
     if (b) return b;
-    return sub_enabled() ? sub_lds_bytes(g) : 0;
+    return sub_enabled(g) ? sub_lds_bytes(g) : 0;
 }
 
 const char *tile_kernel_name(const DevGraph &g) {
     if (tile64_lds_bytes(g)) return "tile_kernel";
-    if (sub_enabled() && sub_lds_bytes(g)) return "tile_sub_kernel";
+    if (sub_enabled(g) && sub_lds_bytes(g)) return "tile_sub_kernel";
     return "";
 }
 
@@ -990,7 +997,7 @@ hipError_t launch_tile_stream(const DevGraph &g, const DevState &st, int max_ite
 hipError_t launch_tile(const DevGraph &g, const DevState &st, int max_iter, bool nllr, hipStream_t s) {
     if (st.ntiles > st.nslots) return hipErrorInvalidValue;
     const size_t lds = tile64_lds_bytes(g);
-    if (!lds) return sub_enabled() ? launch_tile_sub(g, st, max_iter, nllr, s) : hipErrorInvalidValue;
+    if (!lds) return sub_enabled(g) ? launch_tile_sub(g, st, max_iter, nllr, s) : hipErrorInvalidValue;
     tile_kernel<<<st.ntiles, 64 * kTW, lds, s>>>(g, st, max_iter, nllr ? 1 : 0, g.col_idx, g.row_ptr, kAtanhCoef);
     return hipGetLastError();
 }

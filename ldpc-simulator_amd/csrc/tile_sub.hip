@@ -57,6 +57,37 @@ struct SubCfg {
     static constexpr int K = Q == 4 ? 10 : 8;     // slots per lane: row degree <= kSW * Q * K
 };
 
+// LDPC_SUB_PERMLANE 1: the product crosses lane groups by v_permlane16/32_swap
+// (Q = 4), 0: by ds_bpermute.  LDPC_SUB_PRIO 1: raised issue priority while a
+// wavefront carries the chain.  LDPC_SUB_NT: the message stream E (read once,
+// written once per pass) non-temporal, as in tile_kernels.hip.
+#ifndef LDPC_SUB_PERMLANE
+#define LDPC_SUB_PERMLANE 1
+#endif
+#ifndef LDPC_SUB_PRIO
+#define LDPC_SUB_PRIO 1
+#endif
+#ifndef LDPC_SUB_NT
+#define LDPC_SUB_NT 1
+#endif
+// LDPC_SUB_HOPFIRST 1: body(r) = hop(r), P3(r-1), P1(r+1): the chain of row r
+// runs while the other wavefronts are still in P3(r-1) (its S additions then
+// wait on per-row P3 completion counts, and chain slots are reused every 4
+// rows); 0: P3(r-1), hop(r), P1(r+1) (S order by program order, 2 slots).
+#ifndef LDPC_SUB_HOPFIRST
+#define LDPC_SUB_HOPFIRST 1
+#endif
+constexpr int kSR = LDPC_SUB_HOPFIRST ? 4 : 2;  // chain slots
+__device__ __forceinline__ double ld_sub_msg(const double *p) {
+    return LDPC_SUB_NT ? __builtin_nontemporal_load(p) : *p;
+}
+__device__ __forceinline__ void st_sub_msg(double *p, double v) {
+    if (LDPC_SUB_NT)
+        __builtin_nontemporal_store(v, p);
+    else
+        *p = v;
+}
+
 struct SubLayout {
     size_t S, math, slot, zb, ib, lane_i, flags, dummy, total;
 };
@@ -67,16 +98,16 @@ __host__ __device__ inline SubLayout sub_layout(int k, int m, int F) {
     o = al16(o + (size_t)k * F * sizeof(double));
     t.math = o;
     o = al16(o + sizeof(MathLds));
-    t.slot = o;  // [2][F] chain slots
-    o = al16(o + 2 * (size_t)F * sizeof(double));
+    t.slot = o;  // [kSR][F] chain slots
+    o = al16(o + kSR * (size_t)F * sizeof(double));
     t.zb = o;  // [kw][F] z^1 bits of the A columns
     o = al16(o + (size_t)((k + 31) / 32) * F * sizeof(uint32_t));
     t.ib = o;  // [mw][F] z^1 bits of the identity columns (adjacent to zb)
     o = al16(o + (size_t)((m + 31) / 32) * F * sizeof(uint32_t));
     t.lane_i = o;  // bad[F], nllr count[F], live[F]
     o = al16(o + 3 * (size_t)F * sizeof(int));
-    t.flags = o;  // chain flag[2], tiny[2], tiny sequence, running
-    o = al16(o + 6 * sizeof(int));
+    t.flags = o;  // chain flag[kSR], tiny[kSR], tiny sequence, running, P3 counts[4]
+    o = al16(o + (2 * kSR + 6) * sizeof(int));
     t.dummy = o;  // [F] target of the identity lane's masked-off S update
     o = al16(o + (size_t)F * sizeof(double));
     t.total = o;
@@ -112,10 +143,14 @@ struct SubCtx {
     double *dummy;  // LDS, this lane's frame
     double *slot;   // LDS, chain slot s at [s * F]
     uint32_t *ib;   // LDS, word w at [w * F]
-    int *flag, *tinyf, *tseq;
+    int *flag, *tinyf, *tseq, *p3n;
     LdsTanh ttab;
     LdsLog ltab;
     AtanhCoef ac;
+    // uniform (SGPR) tile bases + this lane's byte offset: every access is a
+    // 32-bit per-lane offset from a scalar base (global_load ... v_off, s_base)
+    const char *Eu, *Lu, *Cu;
+    uint32_t lo8;
     int k, wave, j, f;
     int ep0;
     bool first, live;
@@ -132,9 +167,34 @@ template <int Q>
 __device__ __forceinline__ int sub_edge(const SubCtx<Q> &c, const SubChunk &rc, int i) {
     return rc.c0 + min(c.j * rc.CS + i, rc.cnt - 1);
 }
+// element (item, this lane's frame) of a tile array: item * 64 * 8 + lane * 8 bytes
+template <int Q>
+__device__ __forceinline__ uint32_t sub_off(const SubCtx<Q> &c, int item) {
+    return ((uint32_t)item << 9) + c.lo8;
+}
+template <int Q>
+__device__ __forceinline__ double *sub_e(const SubCtx<Q> &c, int edge) {
+    return (double *)(c.Eu + sub_off(c, edge));
+}
+template <int Q>
+__device__ __forceinline__ double *sub_l(const SubCtx<Q> &c, int col) {
+    return (double *)(c.Lu + sub_off(c, col));
+}
+template <int Q>
+__device__ __forceinline__ const double *sub_c(const SubCtx<Q> &c, int col) {
+    return (const double *)(c.Cu + sub_off(c, col));
+}
+template <int Q>
+__device__ __forceinline__ int sub_col(const SubCtx<Q> &c, int edge) {
+    return *(const int *)((const char *)c.col_idx + ((uint32_t)edge << 2));
+}
 
 // P1: t = tanh((L[col] - E_old)/2) for this lane's slots; returns whether
 // some lane's own edge has |t| <= 1e-10 (:159).
+// P1: t = tanh((L[col] - E_old)/2) for this lane's slots; returns whether
+// some lane's own edge has |t| <= 1e-10 (:159).  E_old is requested first
+// (independent of the column indices), then the indices, then the posterior
+// gather that needs them.
 template <int Q>
 __device__ __forceinline__ bool sub_p1(const SubCtx<Q> &c, const SubChunk &rc, double (&t)[SubCfg<Q>::K]) {
     constexpr int K = SubCfg<Q>::K;
@@ -142,29 +202,63 @@ __device__ __forceinline__ bool sub_p1(const SubCtx<Q> &c, const SubChunk &rc, d
     if (rc.cnt > 0) {
         const int nj = sub_nj(c, rc);
         int col[K];
-#pragma unroll
-        for (int i = 0; i < K; ++i)
-            if (i < rc.CS) col[i] = c.col_idx[sub_edge(c, rc, i)];
         double eo[K];
 #pragma unroll
         for (int i = 0; i < K; ++i) {
             if (i < rc.CS) {
-                t[i] = c.first ? c.Cb[(size_t)col[i] * kTile] : ld_l2(c.Lb + (size_t)col[i] * kTile);
-                eo[i] = c.first ? 0.0 : c.Eb[(size_t)sub_edge(c, rc, i) * kTile];
+                const int e = sub_edge(c, rc, i);
+                eo[i] = c.first ? 0.0 : ld_sub_msg(sub_e(c, e));
+                col[i] = sub_col(c, e);
             }
         }
+        const char *Lsrc = c.first ? c.Cu : c.Lu;  // iteration 0: M = ch (:85-90); uniform
+#pragma unroll
+        for (int i = 0; i < K; ++i)
+            if (i < rc.CS) t[i] = ld_l2((const double *)(Lsrc + sub_off(c, col[i])));
 #pragma unroll
         for (int i = 0; i < K; ++i) {
             if (i < rc.CS) {
                 const double M = c.first ? t[i] : t[i] - eo[i];  // :85-90 / :260-268
                 const double d = M * 0.5;
+#ifdef LDPC_SUB_DIAG_NOMATH  // diagnostic (WRONG results): tanh as one fma
+                t[i] = __builtin_fma(d, 0.0625, 0.25);
+#else
                 const double r = np_tanh(d, c.ttab);
                 t[i] = d > 17.5 ? kCL : (d < -17.5 ? -kCL : r);  // :138-146
+#endif
                 tiny |= i < nj && !(fabs(t[i]) > kTiny);
+                // slots past this lane's piece: 1.0, an exact no-op in the chain product
+                if (i >= nj) t[i] = 1.0;
             }
         }
     }
     return __ballot(tiny) != 0ull;
+}
+
+// Lane-group hand-over for Q = 4 (lane = j*16 + f: group j is DPP row j) with
+// gfx950's v_permlane16_swap / v_permlane32_swap (VALU, no LDS round trip):
+// permlane16_swap(x, x) -> {[x0 x0 x2 x2], [x1 x1 x3 x3]} (rows),
+// permlane32_swap(x, x) -> {[x0 x1 x0 x1], [x2 x3 x2 x3]}.
+__device__ __forceinline__ uint32_t p16(uint32_t x, int which) {
+    const auto r = __builtin_amdgcn_permlane16_swap(x, x, false, false);
+    return which ? r[1] : r[0];
+}
+__device__ __forceinline__ uint32_t p32(uint32_t x, int which) {
+    const auto r = __builtin_amdgcn_permlane32_swap(x, x, false, false);
+    return which ? r[1] : r[0];
+}
+// value of group jj moved into group jj+1 (other groups: don't care)
+__device__ __forceinline__ double group_up4(double v, int jj) {
+    const uint64_t u = dbits(v);
+    uint32_t lo = (uint32_t)u, hi = (uint32_t)(u >> 32);
+    if (jj == 1) {  // row 1 -> row 2: [x0 x1 x0 x1] then its odd rows
+        lo = p16(p32(lo, 0), 1);
+        hi = p16(p32(hi, 0), 1);
+    } else {  // row 0 -> 1, row 2 -> 3
+        lo = p16(lo, 0);
+        hi = p16(hi, 0);
+    }
+    return dfrom(((uint64_t)hi << 32) | lo);
 }
 
 __device__ __forceinline__ double shfl_d(double v, int src) {
@@ -174,13 +268,34 @@ __device__ __forceinline__ double shfl_d(double v, int src) {
     return dfrom(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
 }
 
-// hop: this wavefront's chunk of row r's left-to-right product.
+// P * t[0] * ... * t[n-1] as exactly n dependent multiplies (a uniform branch
+// on n selects a straight-line sequence; slots past a lane's piece hold 1.0)
+template <int K, int N>
+struct SubMul {
+    static __device__ __forceinline__ double run(double P, const double (&t)[K], int n) {
+        if (n == N) {
+#pragma unroll
+            for (int i = 0; i < N; ++i) P = P * t[i];
+            return P;
+        }
+        return SubMul<K, N - 1>::run(P, t, n);
+    }
+};
+template <int K>
+struct SubMul<K, 0> {
+    static __device__ __forceinline__ double run(double P, const double (&)[K], int) { return P; }
+};
+
+// hop: this wavefront's chunk of row r's left-to-right product.  Round jj
+// multiplies lane group jj's slots into the running product (every lane
+// computes; group jj's lanes hold the value that matters) and moves it to
+// group jj+1.
 template <int Q>
 __device__ __forceinline__ void sub_hop(const SubCtx<Q> &c, int r, const double (&t)[SubCfg<Q>::K], bool tiny) {
     constexpr int F = SubCfg<Q>::F, K = SubCfg<Q>::K;
     const SubChunk rc = sub_chunk(c.row_ptr, r, c.wave, Q);
     if (rc.deg == 0) return;  // spa_decoder.py:115-122
-    const int s = r & 1;
+    const int s = r & (kSR - 1);
     const int ep = ((c.ep0 + r) & 0x3ffffff) * 32;
     double *sl = c.slot + s * F;
     double P = 1.0;  // 1.0 * t0 == t0 exactly
@@ -188,15 +303,21 @@ __device__ __forceinline__ void sub_hop(const SubCtx<Q> &c, int r, const double 
         wait_flag(c.flag + s, ep + c.wave);
         P = *sl;
     }
-    const int nj = sub_nj(c, rc);
+    if (LDPC_SUB_PRIO) __builtin_amdgcn_s_setprio(2);
+    int last = -1;
 #pragma unroll
     for (int jj = 0; jj < Q; ++jj) {
-        if (jj * rc.CS < rc.cnt) {  // lane group jj holds edges of this chunk
-            double Pl = P;
-#pragma unroll
-            for (int i = 0; i < K; ++i)
-                if (i < rc.CS) Pl = i < nj ? Pl * t[i] : Pl;
-            P = shfl_d(Pl, jj * F + c.f);
+        if (jj * rc.CS < rc.cnt) {  // lane group jj holds edges of this chunk (uniform)
+            const double Pl = SubMul<K, K>::run(P, t, rc.CS);
+            last = jj;
+            if (jj + 1 < Q && (jj + 1) * rc.CS < rc.cnt) {
+                if (Q == 4 && LDPC_SUB_PERMLANE)
+                    P = group_up4(Pl, jj);
+                else
+                    P = shfl_d(Pl, jj * F + c.f);
+            } else {
+                P = Pl;
+            }
         }
     }
     if ((threadIdx.x & 63) == 0) {
@@ -205,19 +326,20 @@ __device__ __forceinline__ void sub_hop(const SubCtx<Q> &c, int r, const double 
         else if (tiny)
             lds_st(c.tinyf + s, 1);
     }
-    if (c.j == 0) *sl = P;
+    if (c.j == last) *sl = P;
     lds_release();
     if ((threadIdx.x & 63) == 0) lds_st(c.flag + s, ep + c.wave + 1);
+    if (LDPC_SUB_PRIO) __builtin_amdgcn_s_setprio(0);
 }
 
 // P3: E_new of this lane's slots of row r, stored and folded into S; the
 // identity column's posterior and z^1 bit.
 template <int Q>
-__device__ __forceinline__ void sub_p3(SubCtx<Q> &c, int r, double (&t)[SubCfg<Q>::K]) {
+__device__ __forceinline__ void sub_p3_body(SubCtx<Q> &c, int r, double (&t)[SubCfg<Q>::K]) {
     constexpr int F = SubCfg<Q>::F, K = SubCfg<Q>::K;
     const SubChunk rc = sub_chunk(c.row_ptr, r, c.wave, Q);
     if (rc.deg == 0) return;
-    const int s = r & 1;
+    const int s = r & (kSR - 1);
     const int ep = ((c.ep0 + r) & 0x3ffffff) * 32;
     wait_flag(c.flag + s, ep + kSW);
     const bool tiny_row = uniform(lds_ld(c.tinyf + s)) != 0;
@@ -235,8 +357,19 @@ __device__ __forceinline__ void sub_p3(SubCtx<Q> &c, int r, double (&t)[SubCfg<Q
     int col[K];
 #pragma unroll
     for (int i = 0; i < K; ++i)
-        if (i < rc.CS) col[i] = c.col_idx[sub_edge(c, rc, i)];
+        if (i < rc.CS) col[i] = sub_col(c, sub_edge(c, rc, i));
+#ifdef LDPC_SUB_DIAG_NOMATH  // diagnostic (WRONG results): E = clip(P * t)
     if (!tiny_row) {
+#pragma unroll
+        for (int i = 0; i < K; ++i)
+            if (i < rc.CS) t[i] = clip_cl(P * t[i]);
+    } else
+#endif
+    if (!tiny_row && div_nr_ok(P)) {  // the IEEE quotient without the scaling steps (cn_common.h)
+#pragma unroll
+        for (int i = 0; i < K; ++i)
+            if (i < rc.CS) t[i] = 2.0 * atanh_f(clip_cl(div_nr(P, t[i])), c.ltab, c.ac);  // :159-168
+    } else if (!tiny_row) {
 #pragma unroll
         for (int i = 0; i < K; ++i)
             if (i < rc.CS) t[i] = 2.0 * atanh_f(clip_cl(P / t[i]), c.ltab, c.ac);  // :159-168
@@ -276,7 +409,7 @@ __device__ __forceinline__ void sub_p3(SubCtx<Q> &c, int r, double (&t)[SubCfg<Q
     if (c.live) {
 #pragma unroll
         for (int i = 0; i < K; ++i)
-            if (i < rc.CS && i < nj) c.Eb[(size_t)sub_edge(c, rc, i) * kTile] = t[i];
+            if (i < rc.CS && i < nj) st_sub_msg(sub_e(c, sub_edge(c, rc, i)), t[i]);
     }
     // S_col += E_new, rows ascending (a column occurs once per row: no two
     // lanes of a row share (col, frame)); the identity edge goes to `dummy`
@@ -296,8 +429,8 @@ __device__ __forceinline__ void sub_p3(SubCtx<Q> &c, int r, double (&t)[SubCfg<Q
         }
     }
     if (colI >= 0) {  // identity column: L = ch + (0 + E) (:173-185)
-        const double Lj = c.Cb[(size_t)colI * kTile] + (0.0 + EnI);
-        if (c.live) c.Lb[(size_t)colI * kTile] = Lj;
+        const double Lj = *sub_c(c, colI) + (0.0 + EnI);
+        if (c.live) *sub_l(c, colI) = Lj;
         if (!(Lj < 0.0)) {
             const int q = colI - c.k;
             atomicOr(c.ib + (q >> 5) * F, 1u << (q & 31));
@@ -305,11 +438,30 @@ __device__ __forceinline__ void sub_p3(SubCtx<Q> &c, int r, double (&t)[SubCfg<Q
     }
 }
 
+// P3 of row r; in hop-first order its S additions wait until every
+// wavefront's P3 of row r-1 is complete (count per row g = pass*m + r)
+template <int Q>
+__device__ __forceinline__ void sub_p3(SubCtx<Q> &c, int r, double (&t)[SubCfg<Q>::K]) {
+    const int g = c.ep0 + r;
+    if (LDPC_SUB_HOPFIRST && g > 0) wait_ge(c.p3n + ((g - 1) & 3), kSW * (((g - 1) >> 2) + 1));
+    sub_p3_body(c, r, t);
+    if (LDPC_SUB_HOPFIRST) {
+        lds_release();  // this row's S additions before the count
+        if ((threadIdx.x & 63) == 0)
+            __hip_atomic_fetch_add(c.p3n + (g & 3), 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+}
+
 template <int Q>
 __device__ __forceinline__ void sub_body(SubCtx<Q> &c, int r, int m, double (&tcur)[SubCfg<Q>::K], bool ycur,
                                          double (&toth)[SubCfg<Q>::K], bool &yoth) {
-    if (r >= 1) sub_p3(c, r - 1, toth);
-    if (r < m) sub_hop(c, r, tcur, ycur);
+    if (LDPC_SUB_HOPFIRST) {
+        if (r < m) sub_hop(c, r, tcur, ycur);
+        if (r >= 1) sub_p3(c, r - 1, toth);
+    } else {
+        if (r >= 1) sub_p3(c, r - 1, toth);
+        if (r < m) sub_hop(c, r, tcur, ycur);
+    }
     if (r + 1 < m) yoth = sub_p1(c, sub_chunk(c.row_ptr, r + 1, c.wave, Q), toth);
 }
 
@@ -336,8 +488,8 @@ __global__ __launch_bounds__(64 * kSW, 1) void tile_sub_kernel(DevGraph g, DevSt
     for (int i = threadIdx.x; i < g.k * F; i += blockDim.x) S[i] = 0.0;
     for (int i = threadIdx.x; i < (kw + mw) * F; i += blockDim.x) zb[i] = 0u;
     for (int i = threadIdx.x; i < 2 * F; i += blockDim.x) bad[i] = 0;
-    if (threadIdx.x < 4) flags[threadIdx.x] = -1;
-    if (threadIdx.x == 4) flags[4] = 0;
+    if (threadIdx.x < 2 * kSR) flags[threadIdx.x] = -1;
+    if (threadIdx.x >= 2 * kSR && threadIdx.x < 2 * kSR + 6) flags[threadIdx.x] = 0;
     const int lane = threadIdx.x & 63;
     const int wave = uniform(threadIdx.x >> 6);
     const int j = lane / F, f = lane % F;
@@ -353,14 +505,19 @@ __global__ __launch_bounds__(64 * kSW, 1) void tile_sub_kernel(DevGraph g, DevSt
     c.Eb = st.E + (size_t)tile * g.nnz * kTile + lo;
     c.Lb = st.L + (size_t)tile * g.n * kTile + lo;
     c.Cb = st.ch + (size_t)tile * g.n * kTile + lo;
+    c.Eu = (const char *)(st.E + (size_t)tile * g.nnz * kTile);
+    c.Lu = (const char *)(st.L + (size_t)tile * g.n * kTile);
+    c.Cu = (const char *)(st.ch + (size_t)tile * g.n * kTile);
+    c.lo8 = (uint32_t)lo * 8u;
     c.Tb = st.T + (size_t)blockIdx.x * g.max_row_deg * F + f;
     c.S = S + f;
     c.dummy = (double *)(lds + ly.dummy) + f;
     c.slot = (double *)(lds + ly.slot) + f;
     c.ib = ib + f;
     c.flag = flags;
-    c.tinyf = flags + 2;
-    c.tseq = flags + 4;
+    c.tinyf = flags + kSR;
+    c.tseq = flags + 2 * kSR;
+    c.p3n = flags + 2 * kSR + 2;
     c.ttab = LdsTanh{mlds.tanh};
     c.ltab = LdsLog{mlds.log};
     c.ac = ac;
@@ -447,11 +604,11 @@ __global__ __launch_bounds__(64 * kSW, 1) void tile_sub_kernel(DevGraph g, DevSt
                 bad[f] = 0;
                 cntl[f] = 0;
             }
-            if (lane == 0) flags[5] = any != 0ull ? 1 : 0;
+            if (lane == 0) flags[2 * kSR + 1] = any != 0ull ? 1 : 0;
         }
         for (int i = threadIdx.x; i < (kw + mw) * F; i += blockDim.x) zb[i] = 0u;
         __syncthreads();
-        if (!flags[5]) break;
+        if (!flags[2 * kSR + 1]) break;
     }
 }
 

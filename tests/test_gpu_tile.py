@@ -91,8 +91,9 @@ def test_tile_mc_counters_equal_split(gpu_available):
 
 
 # --- sub-tile decoder (tile_sub.hip): the WiMAX 2304 codes, 16 or 8 frames per
-# workgroup, lane groups sharing one wavefront's chunk of a check row; opt-in
-# (LDPC_TILE_SUB=1, read by the library at every decode)
+# workgroup, lane groups sharing one wavefront's chunk of a check row.  The
+# 16-frame form (wimax_2304_0.5) is the default; the 8-frame form (r3/4) is
+# opt-in (LDPC_TILE_SUB=1, read by the library at every decode)
 
 
 @pytest.fixture
@@ -100,10 +101,13 @@ def sub_tile(monkeypatch):
     monkeypatch.setenv("LDPC_TILE_SUB", "1")
 
 
-def test_sub_tile_is_opt_in(gpu_available):
+def test_sub_tile_default_for_half_rate_opt_in_for_three_quarter(gpu_available, monkeypatch):
     from ldpc_amd import _lib
-    dec = _decoder("wimax_2304_0.5", 64)
-    assert _lib.lib().ldpc_tile_kernel_name(dec.graph.handle) == b""
+    monkeypatch.delenv("LDPC_TILE_SUB", raising=False)
+    assert _lib.lib().ldpc_tile_kernel_name(_decoder("wimax_2304_0.5", 64).graph.handle) == b"tile_sub_kernel"
+    assert _lib.lib().ldpc_tile_kernel_name(_decoder("wimax_2304_0.75A", 64).graph.handle) == b""
+    monkeypatch.setenv("LDPC_TILE_SUB", "0")
+    assert _lib.lib().ldpc_tile_kernel_name(_decoder("wimax_2304_0.5", 64).graph.handle) == b""
 
 
 def test_sub_tile_is_the_one_launched(gpu_available, sub_tile):

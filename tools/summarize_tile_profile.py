@@ -38,9 +38,11 @@ def main(src, dst, nnz, frames):
             w.writerow(["split", k, split[k][1], split[k][0], None])
     vn = max((k for k in split if "vn_kernel<" in k), key=lambda k: split[k][1])
     factor = 8.0 * nnz * frames / (split[vn][0] * 1024.0)
-    tk = next(k for k in fetch if "tile_kernel" in k)
+    def is_tile(k):  # tile_kernel (64 frames) or tile_sub_kernel<Q> (16 / 8 frames)
+        return "tile_kernel" in k or "tile_sub_kernel" in k
+    tk = max((k for k in fetch if is_tile(k)), key=lambda k: fetch[k][1])
     stats = {r["Name"]: r for r in csv.DictReader(open(os.path.join(dst, "kernel_stats.csv")))}
-    st = next(v for n, v in stats.items() if "tile_kernel" in n)
+    st = next(v for n, v in stats.items() if is_tile(n))
     rd = fetch[tk][0] * 1024.0 * factor
     wr = write[tk][0] * 1024.0
     out = {"fetch_correction_factor": factor, "factor_source": vn, "frames": frames, "edges": nnz,
