@@ -5,7 +5,9 @@ Mirrors python_ldpc_app/encoder_decoder_data.py:EncoderDecoderData (lines
 _k, _rate, _h_std, _permutation, _h_sparse_cached, _g_transpose.  The GF(2)
 elimination runs natively (ldpc_hstd_build, csrc/hstd_builder.cpp) instead of
 the reference's pure-Python loop (:13-183); the result is the same RREF and
-permutation (pinned by sha256 against the reference in tests/golden/codes).
+permutation (pinned by sha256 against the reference; the per-code data --
+ALIST-derived H, H_std / permutation fingerprints -- ships with the package in
+ldpc_amd/codes/, written by tests/golden/gen_golden.py from the reference).
 Matrices are scipy CSR (the reference wraps the same in SparseMatrix).
 """
 import ctypes
@@ -20,6 +22,7 @@ from ._lib import as_i32, check
 from .alist import read_parity_check_matrix
 
 HERE = os.path.dirname(os.path.abspath(__file__))
+CODES_DIR = os.path.join(HERE, "codes")  # ALIST-derived H + fingerprints of the reference's codes
 
 
 def build_standard_form(H):
@@ -103,8 +106,8 @@ class EncoderDecoderData:
 
 
 def load_committed_code(name, codes_dir=None):
-    """Load a code committed under tests/golden/codes (no ALIST file needed on the GPU box)."""
-    codes_dir = codes_dir or os.path.join(HERE, "..", "..", "tests", "golden", "codes")
+    """Load a code shipped in ldpc_amd/codes (no ALIST file needed on the GPU box)."""
+    codes_dir = codes_dir or CODES_DIR
     z = np.load(os.path.join(codes_dir, f"{name}.npz"), allow_pickle=False)
     m, n = int(z["m"]), int(z["n"])
     H = sparse.csr_matrix((z["h_data"], z["h_indices"], z["h_indptr"]), shape=(m, n))

@@ -30,7 +30,7 @@ def pytest_configure(config):
 
 
 def load_code_npz(name):
-    return np.load(os.path.join(GOLDEN, "codes", f"{name}.npz"), allow_pickle=False)
+    return np.load(os.path.join(PKG_DIR, "ldpc_amd", "codes", f"{name}.npz"), allow_pickle=False)
 
 
 _HSTD = {}

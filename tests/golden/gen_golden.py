@@ -19,7 +19,8 @@ What is captured per frame (reference spa_decoder.py:63-280):
          -- full for BCH, every 97th edge for the larger codes, plus sha256
   nllr   _d_summarize_normalized_llr when the normalized-LLR metric is on
 
-Per code (codes/<name>.npz): the ALIST-derived H (utils.py:21-113) as CSR,
+Per code (ldpc-simulator_amd/ldpc_amd/codes/<name>.npz, shipped with the
+package): the ALIST-derived H (utils.py:21-113) as CSR,
 H_std CSR (full for small codes), the column permutation and sha256
 fingerprints of both.
 
@@ -38,6 +39,7 @@ import numpy as np
 REF_APP = "/root/reference/python_ldpc_app"
 REF_DB = "/root/reference/Channel_Codes_Database"
 HERE = os.path.dirname(os.path.abspath(__file__))
+CODES_OUT = os.path.join(HERE, "..", "..", "ldpc-simulator_amd", "ldpc_amd", "codes")  # shipped with the package
 
 CODES = {
     "BCH_7_4_1_strip": "BCH_7_4_1_strip.alist.txt",
@@ -97,7 +99,7 @@ def load_code(name):
     if name in FULL_HSTD:
         out["hstd_indptr"] = hs.indptr.astype(np.int32)
         out["hstd_indices"] = hs.indices.astype(np.int32)
-    np.savez_compressed(os.path.join(HERE, "codes", f"{name}.npz"), **out)
+    np.savez_compressed(os.path.join(CODES_OUT, f"{name}.npz"), **out)
     return edd
 
 
@@ -234,7 +236,7 @@ def main():
     args = ap.parse_args()
     want = lambda s: args.only is None or s in args.only  # noqa: E731
 
-    os.makedirs(os.path.join(HERE, "codes"), exist_ok=True)
+    os.makedirs(CODES_OUT, exist_ok=True)
     need = set()
     if want("codes") or want("bch"):
         need.add("BCH_7_4_1_strip")

@@ -1,7 +1,7 @@
 """Native GF(2) standard-form builder (csrc/hstd_builder.cpp) vs the reference.
 
 Pins: sha256 of H_std CSR and of the permutation, computed by the reference's
-EncoderDecoderData (encoder_decoder_data.py:186-317) in tests/golden/codes.
+EncoderDecoderData (encoder_decoder_data.py:186-317) in ldpc_amd/codes.
 """
 import numpy as np
 import pytest
