@@ -157,6 +157,23 @@ def max_over_ranks(dist, x, local):
     return x if dist is None else dist.max(x)
 
 
+VALU_PEAK = 256 * 4 * 2.4e9 / 2.0  # wave64 VALU instructions/s (2 cycles each per SIMD)
+
+
+def committed_valu(code, kernel):
+    """VALU wave-instructions per frame-iteration of `kernel` on `code` from the
+    newest committed profile (tools/profile_phys.sh + summarize_phys_profile.py)."""
+    pdir = os.path.join(ROOT, "profiles")
+    best = (None, None)
+    for d in sorted(os.listdir(pdir)) if os.path.isdir(pdir) else []:
+        f = os.path.join(pdir, d, "valu.json")
+        if os.path.exists(f):
+            v = json.load(open(f))
+            if v.get("code") == code and v.get("kernel") == kernel:
+                best = (v["valu_insts_per_frame_iteration"], os.path.relpath(f, ROOT))
+    return best
+
+
 def committed_traffic(nnz, frames, kernel="cn"):
     """HBM bytes per cn_kernel launch from the newest committed PMC pass
     (profiles/*/traffic.json, tools/profile.sh + tools/summarize_profile.py)
@@ -489,6 +506,16 @@ def main():
             out["roofline"] = {"bound": "valu", "kernel": pname, "launches": pl,
                                "avg_launch_ms": pms / max(pl, 1),
                                "note": "state in LDS; HBM traffic is the frame input only"}
+            vi, vsrc = committed_valu(args.code, pname)
+            if vi and pms:
+                # VALU issue roofline: wave-instructions per frame-iteration (committed PMC of the
+                # same kernel and code) x this run's frame-iterations / the kernel's HIP-event time
+                ach = vi * int(local_totals[0, 6]) / (pms / 1e3)
+                out["roofline"].update({"achieved": ach, "peak": VALU_PEAK, "unit": "VALU wave-instr/s",
+                                        "frac": ach / VALU_PEAK, "valu_insts_per_frame_iteration": vi,
+                                        "valu_source": vsrc,
+                                        "peak_model": "256 CUs x 4 SIMDs x 2.4 GHz / 2 cycles per wave64 "
+                                                      "VALU instruction (MI355X_MICROARCH.md)"})
             out["decode_roofline"] = {"phys_ms": pms, "gen_ms": prof["generate"][0]}
         if rank == 0 and world == 1 and args.cpu_seconds > 0:
             out["cpu_baseline"] = cpu_baseline_phys((Hphys, H), k, args, ira_code)

@@ -215,9 +215,8 @@ int ldpc_phys_mc_run(ldpc_decoder *d_std, const ldpc_graph *g_phys, uint64_t see
 #define LDPC_K_NKINDS 8
 int ldpc_profile_enable(ldpc_decoder *d, int enable);
 int ldpc_profile_read(ldpc_decoder *d, double *ms_out, int64_t *launches_out);
-/* Diagnostic builds only (-DLDPC_TILE_TRACE): s_memtime stamps of tile_kernel's
- * phase boundaries (workgroup 0, pass 2, rows 0..63), [16 wavefronts][64 rows][8]
- * uint64; returns the count written, or -1 in normal builds. */
+/* Retired diagnostic (round 1's s_memtime phase trace of tile_kernel, a
+ * separate build): kept for ABI stability, always returns -1. */
 int ldpc_diag_tile_trace(uint64_t *out, int64_t n);
 
 /* ------------------------------------------------ multi-GPU (RCCL, xGMI)

@@ -17,16 +17,7 @@ __device__ __forceinline__ int uniform(int x) { return __builtin_amdgcn_readfirs
 // np.clip(q, -CL, CL) as v_max_f64 + v_min_f64 (2 VALU instead of 2 compares
 // and 4 selects).  Differs from np.clip only for NaN, which a message cannot
 // be for finite or infinite channel LLRs (|t| <= 1, |E| <= 35.04).
-#ifndef LDPC_CLIP_ABS
-#define LDPC_CLIP_ABS 0
-#endif
-__device__ __forceinline__ double clip_cl(double q) {
-#if LDPC_CLIP_ABS  // |q| clipped, sign put back: one constant register pair instead of two
-    return __builtin_copysign(fmin(__builtin_fabs(q), kCL), q);
-#else
-    return fmin(fmax(q, -kCL), kCL);
-#endif
-}
+__device__ __forceinline__ double clip_cl(double q) { return fmin(fmax(q, -kCL), kCL); }
 
 // P / t as the compiler's own f64 division sequence (reciprocal, two Newton
 // steps, quotient, one fma correction -- the operations v_div_fmas_f64 and
@@ -35,10 +26,6 @@ __device__ __forceinline__ double clip_cl(double q) {
 // result is the IEEE quotient, bit for bit, whenever t is normal with
 // |t| < 1 (every t of a non-rare row: 1e-10 < |t| <= CL) and |P| >= 2^-900
 // (callers check the latter per wavefront and divide normally otherwise).
-// LDPC_DIV_NR 0 keeps the plain division everywhere.
-#ifndef LDPC_DIV_NR
-#define LDPC_DIV_NR 1
-#endif
 constexpr double kDivNrMin = 0x1p-900;
 __device__ __forceinline__ double div_nr(double P, double t) {
     const double r0 = __builtin_amdgcn_rcp(t);
@@ -49,7 +36,7 @@ __device__ __forceinline__ double div_nr(double P, double t) {
 }
 // whether every lane of the wavefront may take div_nr for numerator P
 __device__ __forceinline__ bool div_nr_ok(double P) {
-    return LDPC_DIV_NR && __ballot(!(__builtin_fabs(P) >= kDivNrMin)) == 0ull;
+    return __ballot(!(__builtin_fabs(P) >= kDivNrMin)) == 0ull;
 }
 
 // ---- math tables in LDS (9 x 16 tanh pairs + 128 log entries = 6.4 KB)
@@ -84,9 +71,6 @@ __device__ __forceinline__ void fill_math_lds(MathLds &m) {
 
 __device__ __forceinline__ double cn_tanh(double M, const LdsTanh &t) {
     const double d = M * 0.5;  // == M/2.0 bit for bit (power-of-two scale)
-#ifdef LDPC_DIAG_NOMATH  // diagnostic build only: memory pattern without the math
-    return d * 0.25 + 0.5;
-#endif
     return d > 17.5 ? kCL : (d < -17.5 ? -kCL : np_tanh(d, t));
 }
 

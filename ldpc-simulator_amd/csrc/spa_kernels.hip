@@ -62,15 +62,6 @@ constexpr int kPv = LDPC_PV;                 // VN column-sum loads in flight
 #ifndef LDPC_PF
 #define LDPC_PF 4
 #endif
-// Tuning knob (experiments only): LDPC_CN_LDS_PAD=<bytes> of dynamic LDS per
-// cn_kernel block caps its blocks per CU (occupancy) without a rebuild.
-inline size_t cn_lds_pad() {
-    static const size_t pad = [] {
-        const char *e = getenv("LDPC_CN_LDS_PAD");
-        return e ? (size_t)strtoul(e, nullptr, 10) : (size_t)0;
-    }();
-    return pad;
-}
 constexpr int kPf = LDPC_PF;  // edges in flight per wavefront (software pipeline depth)
 
 // LDPC_SPLIT_NT 1: the message array E (streamed once per pass, far larger
@@ -178,11 +169,7 @@ __global__ __launch_bounds__(256, LDPC_CN_WAVES) void cn_kernel(DevGraph g, DevS
                 const double M = es.take(k, e + k);
                 if (e + k < end) {  // wave-uniform
                     const double t = cn_tanh(M, ttab);
-#ifdef LDPC_DIAG_NOMATH
-                    const double En = P * t;
-#else
                     const double En = 2.0 * atanh_f(clip_cl(nr ? div_nr(P, t) : P / t), ltab, ac);
-#endif
                     if (live) st_e(&Et[(e + k) * kTile], En);
                 }
             }
@@ -306,11 +293,7 @@ __global__ __launch_bounds__(64 * kRowW, WPS) void cn_row_kernel(DevGraph g, Dev
 #pragma unroll
     for (int i = 0; i < K; ++i) {
         if (i < cnt) {
-#ifdef LDPC_DIAG_NOMATH
-            const double En = P * t[i];
-#else
             const double En = 2.0 * atanh_f(clip_cl(P / t[i]), ltab, ac);
-#endif
             if (live) st_e(&Et[(c0 + i) * kTile], En);
         }
     }
@@ -678,24 +661,11 @@ bool use_cn_row(const DevGraph &g) {
     return force != 0 && g.max_row_deg <= kRowW * kRowK;
 }
 
-// LDPC_CN_ROW_VARIANT=1 (A/B): all loads at once at 4 waves/SIMD (2 workgroups
-// per CU, 128 VGPRs) instead of 4 load stages at 6 waves/SIMD (3 per CU, 80).
-inline int cn_row_variant() {
-    static const int v = [] {
-        const char *e = getenv("LDPC_CN_ROW_VARIANT");
-        return e ? atoi(e) : 0;
-    }();
-    return v;
-}
-
 template <bool kFirst, bool kStream>
 void launch_cn_row(const DevGraph &g, const DevState &st, int par, hipStream_t s) {
     const unsigned grid = (unsigned)(((st.ntiles + 7) / 8) * 8 * g.m);
     const int *ci = g.col_idx, *rp = g.row_ptr;
-    if (cn_row_variant() == 1)
-        cn_row_kernel<kFirst, kStream, 1, 4><<<grid, 64 * kRowW, 0, s>>>(g, st, par, ci, rp, kAtanhCoef);
-    else
-        cn_row_kernel<kFirst, kStream, 4, 6><<<grid, 64 * kRowW, 0, s>>>(g, st, par, ci, rp, kAtanhCoef);
+    cn_row_kernel<kFirst, kStream, 4, 6><<<grid, 64 * kRowW, 0, s>>>(g, st, par, ci, rp, kAtanhCoef);
 }
 
 hipError_t launch_cn(const DevGraph &g, const DevState &st, int it, hipStream_t s, bool stream) {
@@ -713,11 +683,11 @@ hipError_t launch_cn(const DevGraph &g, const DevState &st, int it, hipStream_t 
     const unsigned grid = (unsigned)(((st.ntiles + 7) / 8) * 8 * bpt);
     const int par = it & 1;
     if (stream)
-        cn_kernel<false, true><<<grid, 256, cn_lds_pad(), s>>>(g, st, bpt, par, g.col_idx, g.row_ptr, kAtanhCoef);
+        cn_kernel<false, true><<<grid, 256, 0, s>>>(g, st, bpt, par, g.col_idx, g.row_ptr, kAtanhCoef);
     else if (it == 0)
-        cn_kernel<true, false><<<grid, 256, cn_lds_pad(), s>>>(g, st, bpt, par, g.col_idx, g.row_ptr, kAtanhCoef);
+        cn_kernel<true, false><<<grid, 256, 0, s>>>(g, st, bpt, par, g.col_idx, g.row_ptr, kAtanhCoef);
     else
-        cn_kernel<false, false><<<grid, 256, cn_lds_pad(), s>>>(g, st, bpt, par, g.col_idx, g.row_ptr, kAtanhCoef);
+        cn_kernel<false, false><<<grid, 256, 0, s>>>(g, st, bpt, par, g.col_idx, g.row_ptr, kAtanhCoef);
     return hipGetLastError();
 }
 

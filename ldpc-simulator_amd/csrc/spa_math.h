@@ -83,12 +83,6 @@ constexpr AtanhCoef kAtanhCoef{1.0 / 13.0, 1.0 / 11.0, 1.0 / 9.0, 1.0 / 7.0, 0.2
 
 // log(x) = hi + lo for a positive normal x.  Accurate away from x ~ 1 (the
 // interval holding 1.0 itself is exact: invc = 1), which is all atanh needs.
-#ifndef LDPC_ATANH_SELECT
-#define LDPC_ATANH_SELECT 0
-#endif
-#ifndef LDPC_L2_INLINE
-#define LDPC_L2_INLINE 0
-#endif
 template <class LogTab>
 __host__ __device__ __forceinline__ void log_hilo(double x, const LogTab &lt, double &hi, double &lo,
                                                   const AtanhCoef &c = kAtanhCoef) {
@@ -111,11 +105,7 @@ __host__ __device__ __forceinline__ void log_hilo(double x, const LogTab &lt, do
     p = __builtin_fma(p, r, c.l5);            // 1/5
     p = __builtin_fma(p, r, c.l4);            // -1/4
     p = __builtin_fma(p, r, c.l3);            // 1/3
-#if LDPC_L2_INLINE
-    p = __builtin_fma(p, r, -0.5);  // == c.l2; -0.5 is an inline f64 operand (no register)
-#else
     p = __builtin_fma(p, r, c.l2);            // -1/2
-#endif
     lo = ((w - hi) + r) + (__builtin_fma(kd, c.ln2lo, t.lo) + r2 * p);
 }
 
@@ -152,14 +142,9 @@ template <class LogTab>
 __host__ __device__ __forceinline__ double atanh_f(double q, const LogTab &lt, const AtanhCoef &c = kAtanhCoef) {
     const double a = __builtin_fabs(q);
     double res;
-#if LDPC_ATANH_SELECT  // both branches straight-line, then a select: no exec-mask juggling
-    const double rs = atanh_small_abs(a, c);
-    {
-#else
     if (a < kAtanhSmall) {
         res = atanh_small_abs(a, c);
     } else {
-#endif
         // atanh(a) = log(y)/2, y = (1+a)/(1-a) carried as y_hi + y_lo:
         // u = 1+a and v = 1-a are rounded, their errors cu, cv exact (u-1, v-1
         // exact); y_hi = faithful u/v (rcp + one Newton step), its residual
@@ -176,9 +161,6 @@ __host__ __device__ __forceinline__ double atanh_f(double q, const LogTab &lt, c
         log_hilo(yh, lt, h, l, c);
         res = 0.5 * (h + (l + corr));
     }
-#if LDPC_ATANH_SELECT
-    res = a < kAtanhSmall ? rs : res;
-#endif
     return dfrom(dbits(res) | (dbits(q) & 0x8000000000000000ull));
 }
 

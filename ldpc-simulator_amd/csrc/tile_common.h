@@ -24,28 +24,13 @@ __device__ __forceinline__ void lds_st(int *p, int v) {
 // waiting for its outstanding global stores.
 __device__ __forceinline__ void lds_release() { __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local"); }
 __device__ __forceinline__ void lds_acquire() { __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local"); }
-// Compile-time knobs (A/B builds only): LDPC_TILE_SLEEP polls with s_sleep 1
-// between flag reads; LDPC_TILE_PRIO raises the wavefront's issue priority
-// while it carries the product chain; LDPC_TILE_DIAG_NOCHAIN (diagnostic,
-// WRONG results) skips every wait to time the pipeline without the chain.
-#ifndef LDPC_TILE_SLEEP
-#define LDPC_TILE_SLEEP 1
-#endif
-#ifndef LDPC_TILE_PRIO
-#define LDPC_TILE_PRIO 0
-#endif
+// Polls sleep (s_sleep 1) between flag reads.
 __device__ __forceinline__ void wait_flag(const int *p, int v) {
-#ifndef LDPC_TILE_DIAG_NOCHAIN
-    while (uniform(lds_ld(p)) != v) {
-        if (LDPC_TILE_SLEEP) __builtin_amdgcn_s_sleep(1);
-    }
-#endif
+    while (uniform(lds_ld(p)) != v) __builtin_amdgcn_s_sleep(1);
     lds_acquire();
 }
 __device__ __forceinline__ void wait_ge(const int *p, int v) {
-    while (uniform(lds_ld(p)) < v) {
-        if (LDPC_TILE_SLEEP) __builtin_amdgcn_s_sleep(1);
-    }
+    while (uniform(lds_ld(p)) < v) __builtin_amdgcn_s_sleep(1);
     lds_acquire();
 }
 // Load through L2 (not this CU's L1): data another wavefront of the workgroup

@@ -62,19 +62,9 @@
 namespace ldpc {
 namespace {
 
-#ifndef LDPC_TILE_WAVES
-#define LDPC_TILE_WAVES 16
-#endif
-constexpr int kTW = LDPC_TILE_WAVES;  // wavefronts per workgroup
+constexpr int kTW = 16;               // wavefronts per workgroup
 constexpr int kTK = 192 / kTW;        // edges per wavefront chunk: row degree <= kTW * kTK = 192
-// LDPC_TILE_HOPFIRST 1: body(r) = hop(r), P3(r-1), P1(r+1) (the chain of row r
-// starts before this wavefront's P3 of row r-1; S order then needs the P3
-// completion count, and chain slots are reused every 4 rows); 0: P3(r-1),
-// hop(r), P1(r+1) (the ordering argument above, 2 slots).
-#ifndef LDPC_TILE_HOPFIRST
-#define LDPC_TILE_HOPFIRST 0
-#endif
-constexpr int kTR = LDPC_TILE_HOPFIRST ? 4 : 2;  // chain slots
+constexpr int kTR = 2;                // chain slots (see the ordering argument above)
 constexpr size_t kTileLdsMax = 163840;
 constexpr int kTKW = 10;  // (z^1)_A words per lane held in registers for the syndrome: k <= 320
 
@@ -97,105 +87,21 @@ __host__ __device__ inline TileLayout tile_layout(int k, int m) {
     o = al16(o + (size_t)((m + 31) / 32) * kTile * sizeof(uint32_t));
     t.lane_i = o;  // bad[64], nllr count[64], live[64]
     o = al16(o + 3 * kTile * sizeof(int));
-    t.flags = o;  // chain flag[kTR], tiny[kTR], tiny sequence, tile running, P3 counts[4]
-    o = al16(o + (2 * kTR + 6) * sizeof(int));
+    t.flags = o;  // chain flag[kTR], tiny[kTR], tiny sequence, tile running
+    o = al16(o + (2 * kTR + 2) * sizeof(int));
     t.total = o;
     return t;
 }
 
-// Compile-time layout/schedule switches (A/B builds; defaults = measured best):
-//   LDPC_TILE_SADDR     1: tile accesses as uniform base + 32-bit byte offset
-//                       (saddr form); 0: per-lane 64-bit pointers
-//   LDPC_TILE_P3FUSED   1: each edge's E_new computed and stored in one loop;
-//                       0: all E_new of the chunk first, then the stores
-//   LDPC_TILE_PREFETCH  1: the next P1's loads are issued inside this P3;
-//                       0: P1 issues its loads after the hop, in STAGES groups
-#ifndef LDPC_TILE_SADDR
-#define LDPC_TILE_SADDR 0
-#endif
-#ifndef LDPC_TILE_P3FUSED
-#define LDPC_TILE_P3FUSED 0
-#endif
-#ifndef LDPC_TILE_PREFETCH
-#define LDPC_TILE_PREFETCH 0
-#endif
-#ifndef LDPC_TILE_STAGES
-#define LDPC_TILE_STAGES 1
-#endif
-//   LDPC_TILE_TANH_BF   1: tanh evaluated for every lane, the +-17.5 clip as
-//                       selects (straight-line code across the chunk's edges)
-//   LDPC_TILE_SMALLQ    1: all q = clip(P/t) of the chunk first; if no lane of
-//                       the wavefront has |q| >= 2^-5 (every edge at 0 dB),
-//                       the whole chunk takes atanh's Taylor branch as one
-//                       straight-line block, else atanh_f per edge
-#ifndef LDPC_TILE_TANH_BF
-#define LDPC_TILE_TANH_BF 1
-#endif
-#ifndef LDPC_TILE_SMALLQ
-#define LDPC_TILE_SMALLQ 0
-#endif
-//   LDPC_TILE_GROUP     edges per straight-line group in the P1 / P3 math
-//   LDPC_TILE_STORE1    1: P3 stores the chunk's E_new in one live-masked
-//                       block (one exec-mask switch per chunk, not per edge)
-#ifndef LDPC_TILE_STORE1
-#define LDPC_TILE_STORE1 1
-#endif
-#ifndef LDPC_TILE_GROUP
-#define LDPC_TILE_GROUP 1
-#endif
-constexpr int kTG = LDPC_TILE_GROUP;
-//   LDPC_TILE_DIVNR     P3's P / t as cn_common.h div_nr (bit-identical):
-//                       0 off, 1 per-wavefront branch around the group loop,
-//                       2 per-edge select between div_nr and P / t
-#ifndef LDPC_TILE_DIVNR
-#define LDPC_TILE_DIVNR 0
-#endif
-//   LDPC_TILE_CONST_COEF 1: atanh coefficients as compile-time constants
-//                       instead of kernel-argument SGPRs
-#ifndef LDPC_TILE_CONST_COEF
-#define LDPC_TILE_CONST_COEF 0
-#endif
-//   LDPC_TILE_NT        bit 0: E_old loads, bit 1: E_new stores as non-temporal
-//                       accesses: the message stream (read once, written once
-//                       per iteration) then does not evict the tile's
-//                       posteriors (the L[col] gather) from L2
-#ifndef LDPC_TILE_NT
-#define LDPC_TILE_NT 3
-#endif
-__device__ __forceinline__ double ld_msg(const double *p) {
-    return (LDPC_TILE_NT & 1) ? __builtin_nontemporal_load(p) : *p;
-}
-__device__ __forceinline__ void st_msg(double *p, double v) {
-    if (LDPC_TILE_NT & 2)
-        __builtin_nontemporal_store(v, p);
-    else
-        *p = v;
-}
-
-// LDPC_TILE_TRACE (diagnostic build): s_memtime stamps of every wavefront of
-// workgroup 0 at the phase boundaries of rows 0..kTrRows-1 of pass 2, read
-// back with ldpc_diag_tile_trace (ldpc_api.cpp); tools/tile_trace.py.
-#ifdef LDPC_TILE_TRACE
-constexpr int kTrRows = 64, kTrEv = 8;
-__device__ unsigned long long g_tile_trace[kTW][kTrRows][kTrEv];
-#define TSTAMP(c, r, ev)                                                                              \
-    do {                                                                                              \
-        if (blockIdx.x == 0 && (c).ep0 == 2 * (c).m_ && (r) < kTrRows && (c).lane == 0)               \
-            g_tile_trace[(c).wave][(r)][(ev)] = __builtin_amdgcn_s_memtime();                         \
-    } while (0)
-#else
-#define TSTAMP(c, r, ev) \
-    do {                 \
-    } while (0)
-#endif
+// The message stream (E_old loads, E_new stores) is non-temporal: read once and
+// written once per pass, it then does not evict the tile's posteriors (the
+// L[col] gather) from L2 (profiles/r1u_nt).
+__device__ __forceinline__ double ld_msg(const double *p) { return __builtin_nontemporal_load(p); }
+__device__ __forceinline__ void st_msg(double *p, double v) { __builtin_nontemporal_store(v, p); }
 
 // element (item, lane) of a tile array
 template <class T>
 __device__ __forceinline__ T *at(T *base, int item, uint32_t lane) {
-    if (LDPC_TILE_SADDR) {
-        const uint32_t off = ((uint32_t)item * kTile + lane) * (uint32_t)sizeof(T);
-        return (T *)((char *)base + off);
-    }
     return base + (size_t)item * kTile + lane;
 }
 
@@ -223,14 +129,13 @@ struct TileCtx {
     double *S;         // LDS [k][64]
     double *slot;      // LDS [kTR][64]
     uint32_t *ib;      // LDS [mw][64] z^1 of the identity columns
-    int *flag, *tinyf, *tseq, *p3n;
+    int *flag, *tinyf, *tseq;
     LdsTanh ttab;
     LdsLog ltab;
     AtanhCoef ac;
     int k, wave;
     uint32_t lane;
     int ep0;  // epoch of row 0 in this pass (flags are tagged (epoch, stage))
-    int m_;   // rows (trace builds)
     bool first, live;
     bool fresh;  // streaming: this lane's frame is on its first pass (M = L - 0)
     int ntiny;
@@ -238,82 +143,40 @@ struct TileCtx {
 
 // P1 pieces: L[col] of edge i of chunk rc, E_old, and t = tanh((L - E_old)/2).
 // Loads are unconditional (index clamped into the chunk).
-// LDPC_TILE_DIAG_NOLOAD_L / _E (diagnostic builds, WRONG results): replace the
-// posterior gather / the E_old stream by a register value to time the rest.
 __device__ __forceinline__ double tile_load_l(const TileCtx &c, const RowChunk &rc, int i) {
-#ifdef LDPC_TILE_DIAG_NOLOAD_L
-    return 3.0 + (double)(int)(c.lane + i) * 0.0078125;  // |M| stays away from 0 (no rare rows)
-#endif
     const double *Ls = c.first ? c.Cb : c.Lb;
     return ld_l2(at(Ls, c.col_idx[rc.c0 + min(i, rc.cnt - 1)], c.lane));
 }
 __device__ __forceinline__ double tile_load_e(const TileCtx &c, const RowChunk &rc, int i) {
-#ifdef LDPC_TILE_DIAG_NOLOAD_E
-    return (double)(int)(c.lane + i) * 0.0625;
-#endif
     return c.first ? 0.0 : ld_msg(at(c.Eb, rc.c0 + min(i, rc.cnt - 1), c.lane));
 }
 __device__ __forceinline__ bool tile_t(const TileCtx &c, double &t, double eo) {
     const double M = c.first ? t : t - (c.fresh ? 0.0 : eo);  // :85-90 / :260-268
-#ifdef LDPC_TILE_DIAG_NOTANH  // diagnostic (WRONG results): tanh as one fma
-    t = __builtin_fma(M, 0.125, 0.25);
-    return false;
-#endif
-    if (LDPC_TILE_TANH_BF) {
-        const double d = M * 0.5;
-        const double r = np_tanh(d, c.ttab);
-#if LDPC_CLIP_ABS
-        t = __builtin_fabs(d) > 17.5 ? __builtin_copysign(kCL, d) : r;  // :138-146 (cn_tanh, as selects)
-#else
-        t = d > 17.5 ? kCL : (d < -17.5 ? -kCL : r);  // :138-146 (cn_tanh, as selects)
-#endif
-    } else {
-        t = cn_tanh(M, c.ttab);
-    }
+    // tanh evaluated for every lane, the +-17.5 clip as selects (straight-line
+    // code across the chunk's edges)
+    const double d = M * 0.5;
+    const double r = np_tanh(d, c.ttab);
+    t = d > 17.5 ? kCL : (d < -17.5 ? -kCL : r);  // :138-146 (cn_tanh, as selects)
     return !(fabs(t) > kTiny);
 }
 
-// P1 with its own loads, in STAGES groups; returns whether some lane has
-// |t| <= 1e-10.
+// P1: loads of the chunk, then t = tanh((L - E_old)/2) edge by edge; returns
+// whether some lane has |t| <= 1e-10.
 __device__ __forceinline__ bool tile_p1(const TileCtx &c, const RowChunk &rc, double (&t)[kTK]) {
     bool tiny = false;
     if (rc.cnt > 0) {
-        constexpr int H = (kTK + LDPC_TILE_STAGES - 1) / LDPC_TILE_STAGES;
+        double eo[kTK];
 #pragma unroll
-        for (int h = 0; h < LDPC_TILE_STAGES; ++h) {
-            double eo[H];
-#pragma unroll
-            for (int g0 = h * H; g0 < min((h + 1) * H, kTK); g0 += kTG) {
-                if (g0 < rc.cnt) {
-#pragma unroll
-                    for (int i = g0; i < min(g0 + kTG, min((h + 1) * H, kTK)); ++i) {
-                        t[i] = tile_load_l(c, rc, i);
-                        eo[i - h * H] = tile_load_e(c, rc, i);
-                    }
-                }
-            }
-            // edges in groups of kTG as straight-line code (independent
-            // dependency chains the scheduler can interleave); a group's slots
-            // past the chunk hold the clamped last edge and are never used
-#pragma unroll
-            for (int g0 = h * H; g0 < min((h + 1) * H, kTK); g0 += kTG) {
-                if (g0 < rc.cnt) {
-#pragma unroll
-                    for (int i = g0; i < min(g0 + kTG, min((h + 1) * H, kTK)); ++i)
-                        tiny |= tile_t(c, t[i], eo[i - h * H]);
-                }
+        for (int i = 0; i < kTK; ++i) {
+            if (i < rc.cnt) {
+                t[i] = tile_load_l(c, rc, i);
+                eo[i] = tile_load_e(c, rc, i);
             }
         }
-    }
-    return __ballot(tiny) != 0ull;
-}
-// P1 math on prefetched loads (LDPC_TILE_PREFETCH)
-__device__ __forceinline__ bool tile_p1_math(const TileCtx &c, const RowChunk &rc, double (&t)[kTK],
-                                             const double (&eo)[kTK]) {
-    bool tiny = false;
 #pragma unroll
-    for (int i = 0; i < kTK; ++i)
-        if (i < rc.cnt) tiny |= tile_t(c, t[i], eo[i]);
+        for (int i = 0; i < kTK; ++i)
+            if (i < rc.cnt) tiny |= tile_t(c, t[i], eo[i]);
+    }
     return __ballot(tiny) != 0ull;
 }
 
@@ -338,9 +201,6 @@ template <>
 struct ChainMul<0> {
     static __device__ __forceinline__ double run(double P, const double (&)[kTK], int) { return P; }
 };
-#ifndef LDPC_TILE_CHAINSW
-#define LDPC_TILE_CHAINSW 1
-#endif
 
 // hop: this wavefront's segment of row r's left-to-right product.
 __device__ __forceinline__ void tile_hop(const TileCtx &c, int r, const double (&t)[kTK], bool tiny) {
@@ -350,128 +210,34 @@ __device__ __forceinline__ void tile_hop(const TileCtx &c, int r, const double (
     const int ep = ((c.ep0 + r) & 0x3ffffff) * 32;
     double *sl = c.slot + s * kTile + c.lane;
     double P;
-    if (LDPC_TILE_PRIO) __builtin_amdgcn_s_setprio(2);
     if (c.wave == 0) {
-        if (LDPC_TILE_CHAINSW) {
-            P = ChainMul<kTK>::run(1.0, t, rc.cnt);  // 1.0 * t0 == t0 exactly
-        } else {
-            P = t[0];  // wavefront 0 always holds the row's first edge
-#pragma unroll
-            for (int i = 1; i < kTK; ++i)
-                if (i < rc.cnt) P = P * t[i];
-        }
+        P = ChainMul<kTK>::run(1.0, t, rc.cnt);  // 1.0 * t0 == t0 exactly
         if (c.lane == 0) lds_st(c.tinyf + s, tiny ? 1 : 0);
     } else {
-        TSTAMP(c, r, 3);
         wait_flag(c.flag + s, ep + c.wave);
-        TSTAMP(c, r, 4);
-        P = *sl;
-        if (LDPC_TILE_CHAINSW) {
-            P = ChainMul<kTK>::run(P, t, rc.cnt);
-        } else {
-#pragma unroll
-            for (int i = 0; i < kTK; ++i)
-                if (i < rc.cnt) P = P * t[i];
-        }
+        P = ChainMul<kTK>::run(*sl, t, rc.cnt);
         if (tiny && c.lane == 0) lds_st(c.tinyf + s, 1);
     }
     *sl = P;
     lds_release();
     if (c.lane == 0) lds_st(c.flag + s, ep + c.wave + 1);
-    TSTAMP(c, r, 5);
-    if (LDPC_TILE_PRIO) __builtin_amdgcn_s_setprio(0);
 }
 
 // P3: E_new of this wavefront's chunk of row r, stored and folded into the
-// column sums (t is overwritten with E_new).  With LDPC_TILE_PREFETCH, as
-// slot i of t is consumed the L[col] load of edge i of the next P1 chunk rc1
-// is issued into it (E_old of rc1 into eo first).
-__device__ __forceinline__ void tile_p3(TileCtx &c, int r, double (&t)[kTK], const RowChunk &rc1,
-                                        double (&eo)[kTK]) {
+// column sums (t is overwritten with E_new).
+__device__ __forceinline__ void tile_p3(TileCtx &c, int r, double (&t)[kTK]) {
     const RowChunk rc = chunk_of(c.row_ptr, r, c.wave);
-    const bool pf = LDPC_TILE_PREFETCH && rc1.cnt > 0;
-    if (pf) {
-#pragma unroll
-        for (int i = 0; i < kTK; ++i) eo[i] = tile_load_e(c, rc1, i);
-    }
-    // hop-first order: S additions of row r wait for every wavefront's P3 of
-    // row r-1 (per-slot completion counts, rows by global index g)
-    const int g = c.ep0 + r;
-    if (LDPC_TILE_HOPFIRST && g > 0) wait_ge(c.p3n + ((g - 1) & 3), kTW * (((g - 1) >> 2) + 1));
-    if (rc.deg == 0) {
-        if (pf) {
-#pragma unroll
-            for (int i = 0; i < kTK; ++i) t[i] = tile_load_l(c, rc1, i);
-        }
-        if (LDPC_TILE_HOPFIRST && c.lane == 0)
-            __hip_atomic_fetch_add(c.p3n + (g & 3), 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        return;
-    }
+    if (rc.deg == 0) return;
     const int s = r & (kTR - 1);
     const int ep = ((c.ep0 + r) & 0x3ffffff) * 32;
-    TSTAMP(c, r, 0);
     wait_flag(c.flag + s, ep + kTW);
-    TSTAMP(c, r, 1);
     const double P = c.slot[s * kTile + c.lane];
     const bool tiny_row = uniform(lds_ld(c.tinyf + s)) != 0;
-    const bool fused = LDPC_TILE_P3FUSED && !tiny_row;
-    if (!tiny_row && !LDPC_TILE_P3FUSED && LDPC_TILE_SMALLQ) {
-        bool big = false;
+    if (!tiny_row) {
 #pragma unroll
-        for (int g0 = 0; g0 < kTK; g0 += kTG) {
-            if (g0 < rc.cnt) {
-#pragma unroll
-                for (int i = g0; i < min(g0 + kTG, kTK); ++i) {
-                    t[i] = clip_cl(P / t[i]);  // q (:159-167)
-                    big |= !(fabs(t[i]) < kAtanhSmall) && i < rc.cnt;
-                }
-            }
-        }
-        if (__ballot(big) == 0ull) {
-#pragma unroll
-            for (int g0 = 0; g0 < kTK; g0 += kTG)
-                if (g0 < rc.cnt) {
-#pragma unroll
-                    for (int i = g0; i < min(g0 + kTG, kTK); ++i) t[i] = 2.0 * atanh_small(t[i], c.ac);  // :168
-                }
-        } else {
-#pragma unroll
-            for (int i = 0; i < kTK; ++i)
-                if (i < rc.cnt) t[i] = 2.0 * atanh_f(t[i], c.ltab, c.ac);
-        }
-    } else if (!tiny_row && !LDPC_TILE_P3FUSED && LDPC_TILE_DIVNR == 1 && div_nr_ok(P)) {
-#pragma unroll
-        for (int g0 = 0; g0 < kTK; g0 += kTG) {
-            if (g0 < rc.cnt) {
-#pragma unroll
-                for (int i = g0; i < min(g0 + kTG, kTK); ++i)
-                    t[i] = 2.0 * atanh_f(clip_cl(div_nr(P, t[i])), c.ltab, c.ac);  // :159-168
-            }
-        }
-    } else if (!tiny_row && !LDPC_TILE_P3FUSED && LDPC_TILE_DIVNR == 2) {
-        const bool nr = div_nr_ok(P);
-#pragma unroll
-        for (int g0 = 0; g0 < kTK; g0 += kTG) {
-            if (g0 < rc.cnt) {
-#pragma unroll
-                for (int i = g0; i < min(g0 + kTG, kTK); ++i)
-                    t[i] = 2.0 * atanh_f(clip_cl(nr ? div_nr(P, t[i]) : P / t[i]), c.ltab, c.ac);  // :159-168
-            }
-        }
-    } else if (!tiny_row && !LDPC_TILE_P3FUSED) {
-#pragma unroll
-        for (int g0 = 0; g0 < kTK; g0 += kTG) {
-            if (g0 < rc.cnt) {
-#pragma unroll
-                for (int i = g0; i < min(g0 + kTG, kTK); ++i)
-#ifdef LDPC_TILE_DIAG_NOP3MATH  // diagnostic (WRONG results): E = clip(P*t)
-                    t[i] = clip_cl(P * t[i]);
-#else
-                    t[i] = 2.0 * atanh_f(clip_cl(P / t[i]), c.ltab, c.ac);  // :159-168
-#endif
-            }
-        }
-    } else if (tiny_row) {
+        for (int i = 0; i < kTK; ++i)
+            if (i < rc.cnt) t[i] = 2.0 * atanh_f(clip_cl(P / t[i]), c.ltab, c.ac);  // :159-168
+    } else {
         // rare: q = prod of the others, in order (np.prod(np.delete(...)), :164)
         const int pos0 = c.wave * rc.C;
 #pragma unroll
@@ -502,8 +268,7 @@ __device__ __forceinline__ void tile_p3(TileCtx &c, int r, double (&t)[kTK], con
             }
         }
     }
-    constexpr bool store1 = LDPC_TILE_STORE1 && !LDPC_TILE_P3FUSED && !LDPC_TILE_PREFETCH;
-    if (store1 && c.live) {  // the chunk's E_new stores under ONE exec mask
+    if (c.live) {  // the chunk's E_new stores under ONE exec mask
 #pragma unroll
         for (int i = 0; i < kTK; ++i)
             if (i < rc.cnt) st_msg(at(c.Eb, rc.c0 + i, c.lane), t[i]);
@@ -511,10 +276,7 @@ __device__ __forceinline__ void tile_p3(TileCtx &c, int r, double (&t)[kTK], con
 #pragma unroll
     for (int i = 0; i < kTK; ++i) {
         if (i < rc.cnt) {
-            if (fused) t[i] = 2.0 * atanh_f(clip_cl(P / t[i]), c.ltab, c.ac);  // :159-168
-            const int e = rc.c0 + i;
-            const int col = c.col_idx[e];
-            if (!store1 && c.live) st_msg(at(c.Eb, e, c.lane), t[i]);
+            const int col = c.col_idx[rc.c0 + i];
             if (col < c.k) {  // S_col += E (rows ascending)
                 double *sp = c.S + col * kTile + c.lane;
                 *sp = *sp + t[i];
@@ -527,35 +289,17 @@ __device__ __forceinline__ void tile_p3(TileCtx &c, int r, double (&t)[kTK], con
                 }
             }
         }
-        if (pf) t[i] = tile_load_l(c, rc1, i);
-    }
-    if (LDPC_TILE_HOPFIRST) {
-        lds_release();  // this row's S additions before the count
-        if (c.lane == 0)
-            __hip_atomic_fetch_add(c.p3n + (g & 3), 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
 }
 
+// body(r) = P3(r-1), hop(r), P1(r+1)
 __device__ __forceinline__ void tile_body(TileCtx &c, int r, int m, double (&tcur)[kTK], bool &ycur,
-                                          double (&toth)[kTK], bool &yoth, double (&eo)[kTK]) {
+                                          double (&toth)[kTK], bool &yoth) {
     RowChunk rc1{};
     if (r + 1 < m) rc1 = chunk_of(c.row_ptr, r + 1, c.wave);
-    if (LDPC_TILE_HOPFIRST) {
-        if (r < m) tile_hop(c, r, tcur, ycur);
-        if (r >= 1) tile_p3(c, r - 1, toth, rc1, eo);
-    } else {
-        if (r >= 1) tile_p3(c, r - 1, toth, rc1, eo);
-        if (r >= 1) TSTAMP(c, r - 1, 2);
-        if (r < m) tile_hop(c, r, tcur, ycur);
-    }
-    if (r + 1 < m) {
-        if (LDPC_TILE_PREFETCH && r >= 1) {
-            yoth = tile_p1_math(c, rc1, toth, eo);
-        } else {
-            yoth = tile_p1(c, rc1, toth);
-            TSTAMP(c, r + 1, 6);
-        }
-    }
+    if (r >= 1) tile_p3(c, r - 1, toth);
+    if (r < m) tile_hop(c, r, tcur, ycur);
+    if (r + 1 < m) yoth = tile_p1(c, rc1, toth);
 }
 
 // End of a pass, once every column's z^1 bit is in zb (A part) / ib (identity
@@ -646,7 +390,6 @@ __global__ __launch_bounds__(64 * kTW, 1) void tile_kernel(DevGraph g, DevState 
     for (int i = threadIdx.x; i < 2 * kTile; i += blockDim.x) bad[i] = 0;
     if (threadIdx.x < 2 * kTR) flags[threadIdx.x] = -1;
     if (threadIdx.x == 2 * kTR) flags[2 * kTR] = 0;
-    if (threadIdx.x >= 2 * kTR + 2 && threadIdx.x < 2 * kTR + 6) flags[threadIdx.x] = 0;
     const int lane = threadIdx.x & 63;
     const int wave = uniform(threadIdx.x >> 6);
     const int f = tile * kTile + lane;
@@ -667,15 +410,13 @@ __global__ __launch_bounds__(64 * kTW, 1) void tile_kernel(DevGraph g, DevState 
     c.flag = flags;
     c.tinyf = flags + kTR;
     c.tseq = flags + 2 * kTR;
-    c.p3n = flags + 2 * kTR + 2;
     c.ttab = LdsTanh{mlds.tanh};
     c.ltab = LdsLog{mlds.log};
-    c.ac = LDPC_TILE_CONST_COEF ? kAtanhCoef : ac;
+    c.ac = ac;
     c.k = g.k;
     c.lane = lane;
     c.wave = wave;
     c.ntiny = 0;
-    c.m_ = g.m;
     c.fresh = false;
     const int m = g.m;
 
@@ -683,12 +424,12 @@ __global__ __launch_bounds__(64 * kTW, 1) void tile_kernel(DevGraph g, DevState 
         c.first = it == 0;
         c.live = livel[lane] != 0;
         c.ep0 = it * m;
-        double tA[kTK], tB[kTK], eo[kTK];
+        double tA[kTK], tB[kTK];
         bool yA = false, yB = false;
         if (m > 0) yA = tile_p1(c, chunk_of(row_ptr, 0, wave), tA);
         for (int r = 0; r <= m; r += 2) {
-            tile_body(c, r, m, tA, yA, tB, yB, eo);
-            if (r + 1 <= m) tile_body(c, r + 1, m, tB, yB, tA, yA, eo);
+            tile_body(c, r, m, tA, yA, tB, yB);
+            if (r + 1 <= m) tile_body(c, r + 1, m, tB, yB, tA, yA);
         }
         __syncthreads();  // every P3 done: S complete, identity bits set
 
@@ -780,7 +521,6 @@ __global__ __launch_bounds__(64 * kTW, 1) void tile_stream_kernel(DevGraph g, De
     for (int i = threadIdx.x; i < 2 * kTile; i += blockDim.x) bad[i] = 0;
     if (threadIdx.x < 2 * kTR) flags[threadIdx.x] = -1;
     if (threadIdx.x == 2 * kTR) flags[2 * kTR] = 0;
-    if (threadIdx.x >= 2 * kTR + 2 && threadIdx.x < 2 * kTR + 6) flags[threadIdx.x] = 0;
     const int lane = threadIdx.x & 63;
     const int wave = uniform(threadIdx.x >> 6);
     bool want = true;  // wave 0: this lane asks for a frame
@@ -803,7 +543,6 @@ __global__ __launch_bounds__(64 * kTW, 1) void tile_stream_kernel(DevGraph g, De
     c.flag = flags;
     c.tinyf = flags + kTR;
     c.tseq = flags + 2 * kTR;
-    c.p3n = flags + 2 * kTR + 2;
     c.ttab = LdsTanh{mlds.tanh};
     c.ltab = LdsLog{mlds.log};
     c.ac = ac;
@@ -811,7 +550,6 @@ __global__ __launch_bounds__(64 * kTW, 1) void tile_stream_kernel(DevGraph g, De
     c.lane = lane;
     c.wave = wave;
     c.ntiny = 0;
-    c.m_ = g.m;
     c.first = false;
     const int m = g.m;
     const uint32_t *Ut = st.ubits + (size_t)tile * kw * kTile + lane;
@@ -835,12 +573,12 @@ __global__ __launch_bounds__(64 * kTW, 1) void tile_stream_kernel(DevGraph g, De
         c.live = livel[lane] != 0;
         c.fresh = freshl[lane] != 0;
         c.ep0 = pass * m;
-        double tA[kTK], tB[kTK], eo[kTK];
+        double tA[kTK], tB[kTK];
         bool yA = false, yB = false;
         if (m > 0) yA = tile_p1(c, chunk_of(row_ptr, 0, wave), tA);
         for (int r = 0; r <= m; r += 2) {
-            tile_body(c, r, m, tA, yA, tB, yB, eo);
-            if (r + 1 <= m) tile_body(c, r + 1, m, tB, yB, tA, yA, eo);
+            tile_body(c, r, m, tA, yA, tB, yB);
+            if (r + 1 <= m) tile_body(c, r + 1, m, tB, yB, tA, yA);
         }
         __syncthreads();
 
@@ -921,17 +659,12 @@ __global__ __launch_bounds__(64 * kTW, 1) void tile_stream_kernel(DevGraph g, De
 
 }  // namespace
 
-// diagnostic: copy the trace stamps (LDPC_TILE_TRACE builds; else returns -1)
+// The phase-trace diagnostic build (s_memtime stamps) was retired with the
+// other A/B switches (round 2); the ABI entry reports that.
 int tile_trace_read(unsigned long long *out, size_t n) {
-#ifdef LDPC_TILE_TRACE
-    const size_t b = sizeof(unsigned long long) * (size_t)kTW * kTrRows * kTrEv;
-    if (n * sizeof(unsigned long long) < b) return -1;
-    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_tile_trace), b) == hipSuccess ? (int)(b / 8) : -1;
-#else
     (void)out;
     (void)n;
     return -1;
-#endif
 }
 
 size_t tile64_lds_bytes(const DevGraph &g) {

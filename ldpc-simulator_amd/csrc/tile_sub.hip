@@ -57,36 +57,16 @@ struct SubCfg {
     static constexpr int K = Q == 4 ? 10 : 8;     // slots per lane: row degree <= kSW * Q * K
 };
 
-// LDPC_SUB_PERMLANE 1: the product crosses lane groups by v_permlane16/32_swap
-// (Q = 4), 0: by ds_bpermute.  LDPC_SUB_PRIO 1: raised issue priority while a
-// wavefront carries the chain.  LDPC_SUB_NT: the message stream E (read once,
-// written once per pass) non-temporal, as in tile_kernels.hip.
-#ifndef LDPC_SUB_PERMLANE
-#define LDPC_SUB_PERMLANE 1
-#endif
-#ifndef LDPC_SUB_PRIO
-#define LDPC_SUB_PRIO 1
-#endif
-#ifndef LDPC_SUB_NT
-#define LDPC_SUB_NT 1
-#endif
-// LDPC_SUB_HOPFIRST 1: body(r) = hop(r), P3(r-1), P1(r+1): the chain of row r
-// runs while the other wavefronts are still in P3(r-1) (its S additions then
-// wait on per-row P3 completion counts, and chain slots are reused every 4
-// rows); 0: P3(r-1), hop(r), P1(r+1) (S order by program order, 2 slots).
-#ifndef LDPC_SUB_HOPFIRST
-#define LDPC_SUB_HOPFIRST 1
-#endif
-constexpr int kSR = LDPC_SUB_HOPFIRST ? 4 : 2;  // chain slots
-__device__ __forceinline__ double ld_sub_msg(const double *p) {
-    return LDPC_SUB_NT ? __builtin_nontemporal_load(p) : *p;
-}
-__device__ __forceinline__ void st_sub_msg(double *p, double v) {
-    if (LDPC_SUB_NT)
-        __builtin_nontemporal_store(v, p);
-    else
-        *p = v;
-}
+// The product crosses lane groups by v_permlane16/32_swap (Q = 4) or
+// ds_bpermute (Q = 8); the wavefront carrying the chain runs at raised issue
+// priority; the message stream E (read once, written once per pass) is
+// non-temporal, as in tile_kernels.hip.  Pipeline: body(r) = hop(r), P3(r-1),
+// P1(r+1) -- the chain of row r runs while the other wavefronts are still in
+// P3(r-1); the S additions of a row wait on the per-row P3 completion counts,
+// and the chain slots are reused every 4 rows.
+constexpr int kSR = 4;  // chain slots
+__device__ __forceinline__ double ld_sub_msg(const double *p) { return __builtin_nontemporal_load(p); }
+__device__ __forceinline__ void st_sub_msg(double *p, double v) { __builtin_nontemporal_store(v, p); }
 
 struct SubLayout {
     size_t S, math, slot, zb, ib, lane_i, flags, dummy, total;
@@ -220,12 +200,8 @@ __device__ __forceinline__ bool sub_p1(const SubCtx<Q> &c, const SubChunk &rc, d
             if (i < rc.CS) {
                 const double M = c.first ? t[i] : t[i] - eo[i];  // :85-90 / :260-268
                 const double d = M * 0.5;
-#ifdef LDPC_SUB_DIAG_NOMATH  // diagnostic (WRONG results): tanh as one fma
-                t[i] = __builtin_fma(d, 0.0625, 0.25);
-#else
                 const double r = np_tanh(d, c.ttab);
                 t[i] = d > 17.5 ? kCL : (d < -17.5 ? -kCL : r);  // :138-146
-#endif
                 tiny |= i < nj && !(fabs(t[i]) > kTiny);
                 // slots past this lane's piece: 1.0, an exact no-op in the chain product
                 if (i >= nj) t[i] = 1.0;
@@ -303,7 +279,7 @@ __device__ __forceinline__ void sub_hop(const SubCtx<Q> &c, int r, const double 
         wait_flag(c.flag + s, ep + c.wave);
         P = *sl;
     }
-    if (LDPC_SUB_PRIO) __builtin_amdgcn_s_setprio(2);
+    __builtin_amdgcn_s_setprio(2);
     int last = -1;
 #pragma unroll
     for (int jj = 0; jj < Q; ++jj) {
@@ -311,7 +287,7 @@ __device__ __forceinline__ void sub_hop(const SubCtx<Q> &c, int r, const double 
             const double Pl = SubMul<K, K>::run(P, t, rc.CS);
             last = jj;
             if (jj + 1 < Q && (jj + 1) * rc.CS < rc.cnt) {
-                if (Q == 4 && LDPC_SUB_PERMLANE)
+                if (Q == 4)
                     P = group_up4(Pl, jj);
                 else
                     P = shfl_d(Pl, jj * F + c.f);
@@ -329,7 +305,7 @@ __device__ __forceinline__ void sub_hop(const SubCtx<Q> &c, int r, const double 
     if (c.j == last) *sl = P;
     lds_release();
     if ((threadIdx.x & 63) == 0) lds_st(c.flag + s, ep + c.wave + 1);
-    if (LDPC_SUB_PRIO) __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_s_setprio(0);
 }
 
 // P3: E_new of this lane's slots of row r, stored and folded into S; the
@@ -358,13 +334,6 @@ __device__ __forceinline__ void sub_p3_body(SubCtx<Q> &c, int r, double (&t)[Sub
 #pragma unroll
     for (int i = 0; i < K; ++i)
         if (i < rc.CS) col[i] = sub_col(c, sub_edge(c, rc, i));
-#ifdef LDPC_SUB_DIAG_NOMATH  // diagnostic (WRONG results): E = clip(P * t)
-    if (!tiny_row) {
-#pragma unroll
-        for (int i = 0; i < K; ++i)
-            if (i < rc.CS) t[i] = clip_cl(P * t[i]);
-    } else
-#endif
     if (!tiny_row && div_nr_ok(P)) {  // the IEEE quotient without the scaling steps (cn_common.h)
 #pragma unroll
         for (int i = 0; i < K; ++i)
@@ -443,25 +412,18 @@ __device__ __forceinline__ void sub_p3_body(SubCtx<Q> &c, int r, double (&t)[Sub
 template <int Q>
 __device__ __forceinline__ void sub_p3(SubCtx<Q> &c, int r, double (&t)[SubCfg<Q>::K]) {
     const int g = c.ep0 + r;
-    if (LDPC_SUB_HOPFIRST && g > 0) wait_ge(c.p3n + ((g - 1) & 3), kSW * (((g - 1) >> 2) + 1));
+    if (g > 0) wait_ge(c.p3n + ((g - 1) & 3), kSW * (((g - 1) >> 2) + 1));
     sub_p3_body(c, r, t);
-    if (LDPC_SUB_HOPFIRST) {
-        lds_release();  // this row's S additions before the count
-        if ((threadIdx.x & 63) == 0)
-            __hip_atomic_fetch_add(c.p3n + (g & 3), 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    }
+    lds_release();  // this row's S additions before the count
+    if ((threadIdx.x & 63) == 0)
+        __hip_atomic_fetch_add(c.p3n + (g & 3), 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
 template <int Q>
 __device__ __forceinline__ void sub_body(SubCtx<Q> &c, int r, int m, double (&tcur)[SubCfg<Q>::K], bool ycur,
                                          double (&toth)[SubCfg<Q>::K], bool &yoth) {
-    if (LDPC_SUB_HOPFIRST) {
-        if (r < m) sub_hop(c, r, tcur, ycur);
-        if (r >= 1) sub_p3(c, r - 1, toth);
-    } else {
-        if (r >= 1) sub_p3(c, r - 1, toth);
-        if (r < m) sub_hop(c, r, tcur, ycur);
-    }
+    if (r < m) sub_hop(c, r, tcur, ycur);
+    if (r >= 1) sub_p3(c, r - 1, toth);
     if (r + 1 < m) yoth = sub_p1(c, sub_chunk(c.row_ptr, r + 1, c.wave, Q), toth);
 }
 
