@@ -13,7 +13,10 @@ are fixed and the GPU frames are seeded).  Per-frame outcomes follow main.py
 (:130-138): a frame fails iff its syndrome is non-zero after the last
 iteration, and BER counts u != z^1 bits of failed frames only.
 
-Run on the GPU box:  python tests/ber_overlay.py   (prints the overlay table)
+Run on the GPU box:  python tests/ber_overlay.py [code]   (prints the overlay table)
+Reference curves: wimax_576_0.5 (5 points, 96-384 frames each) and the
+north-star code wimax_2304_0.5 (1.0 / 2.0 / 3.0 dB, 8 / 16 / 64 frames: a 2304
+frame-iteration costs the reference ~25 s of one core).
 """
 import json
 import os
@@ -27,13 +30,13 @@ for p in (os.path.join(ROOT, "ldpc-simulator_amd"), HERE, os.path.join(ROOT, "or
     if p not in sys.path:
         sys.path.insert(0, p)
 
-REF = os.path.join(HERE, "golden", "ber_curve_wimax_576_0.5.json")
+REF_FMT = os.path.join(HERE, "golden", "ber_curve_{}.json")
 SEED = 20260213
 GROUPS = 400
 
 
-def load_reference():
-    return json.load(open(REF))
+def load_reference(code="wimax_576_0.5"):
+    return json.load(open(REF_FMT.format(code)))
 
 
 def gpu_groups(dec, snr_db, B, G, max_iter, seed=SEED, snr_point=0):
@@ -56,10 +59,10 @@ def gpu_groups(dec, snr_db, B, G, max_iter, seed=SEED, snr_point=0):
     return failed.reshape(G, B).sum(1), err.reshape(G, B).sum(1)
 
 
-def overlay(dec, ref=None, groups=GROUPS, q=0.005):
+def overlay(dec, ref=None, groups=GROUPS, q=0.005, code="wimax_576_0.5"):
     """One row per reference point: reference FER/BER, the GPU's pooled values
     and the [q, 1-q] quantiles of its group FER/BER at the reference's B."""
-    ref = ref or load_reference()
+    ref = ref or load_reference(code)
     k = dec.graph.k
     T = int(ref["max_iter"])
     rows = []
@@ -83,8 +86,9 @@ def main():
     from ldpc_amd.device import Decoder, Graph
     if ldpc_amd.device_count() <= 0:
         raise SystemExit("needs a GPU")
-    dec = Decoder(Graph(hstd_for("wimax_576_0.5")), 65536)
-    rows = overlay(dec)
+    code = sys.argv[1] if len(sys.argv) > 1 else "wimax_576_0.5"
+    dec = Decoder(Graph(hstd_for(code)), 16384)
+    rows = overlay(dec, code=code)
     print("| SNR dB | B | FER ref | FER GPU (pooled) | GPU 99% band at B | BER ref | BER GPU (pooled) | GPU 99% band at B |")
     print("|---|---|---|---|---|---|---|---|")
     for r in rows:

@@ -25,3 +25,21 @@ def test_ber_curve_overlays_reference(gpu_available):
     # the curve falls: FER strictly decreasing over 1.0 -> 3.0 dB on the GPU
     fers = [r["fer_gpu"] for r in rows]
     assert all(a > b for a, b in zip(fers, fers[1:])), fers
+
+
+def test_ber_curve_overlays_reference_north_star_code(gpu_available):
+    """The same overlay on wimax_2304_0.5 (BASELINE config 3's code) at
+    1.0 / 2.0 / 3.0 dB against the reference's own main.py run."""
+    import ber_overlay
+    from conftest import hstd_for
+    from ldpc_amd.device import Decoder, Graph
+
+    dec = Decoder(Graph(hstd_for("wimax_2304_0.5"), device=0), 12800)
+    rows = ber_overlay.overlay(dec, groups=200, code="wimax_2304_0.5")
+    assert [r["snr_db"] for r in rows] == [1.0, 2.0, 3.0]
+    for r in rows:
+        print(r)
+        assert r["fer_lo"] <= r["fer_ref"] <= r["fer_hi"], r
+        assert r["ber_lo"] <= r["ber_ref"] <= r["ber_hi"], r
+    fers = [r["fer_gpu"] for r in rows]
+    assert all(a > b for a, b in zip(fers, fers[1:])), fers
