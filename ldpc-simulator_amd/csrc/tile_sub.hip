@@ -68,9 +68,15 @@ constexpr int kSR = 4;  // chain slots
 __device__ __forceinline__ double ld_sub_msg(const double *p) { return __builtin_nontemporal_load(p); }
 __device__ __forceinline__ void st_sub_msg(double *p, double v) { __builtin_nontemporal_store(v, p); }
 
+// Column indices of the rows in flight, staged per wavefront in LDS as 16-bit
+// values one row ahead of their P1 (a ring of 3 rows: P3(r-1), P1(r+1) and the
+// staging of row r+2 in body(r)), so neither P1's posterior gather nor P3 waits
+// on an index load from L2.
+constexpr int kCRing = 3;
 struct SubLayout {
-    size_t S, math, slot, zb, ib, lane_i, flags, dummy, total;
+    size_t S, math, slot, zb, ib, lane_i, flags, dummy, cidx, total;
 };
+__host__ __device__ constexpr int sub_k(int F) { return F == 16 ? SubCfg<4>::K : SubCfg<8>::K; }
 __host__ __device__ inline SubLayout sub_layout(int k, int m, int F) {
     SubLayout t;
     size_t o = 0;
@@ -90,6 +96,8 @@ __host__ __device__ inline SubLayout sub_layout(int k, int m, int F) {
     o = al16(o + (2 * kSR + 6) * sizeof(int));
     t.dummy = o;  // [F] target of the identity lane's masked-off S update
     o = al16(o + (size_t)F * sizeof(double));
+    t.cidx = o;  // [kCRing][kSW][64/F * K] uint16 column indices (one wavefront chunk per row)
+    o = al16(o + (size_t)kCRing * kSW * (64 / F) * sub_k(F) * sizeof(uint16_t));
     t.total = o;
     return t;
 }
@@ -123,6 +131,8 @@ struct SubCtx {
     double *dummy;  // LDS, this lane's frame
     double *slot;   // LDS, chain slot s at [s * F]
     uint32_t *ib;   // LDS, word w at [w * F]
+    uint16_t *cidx; // LDS, this wavefront's index ring: row slot s, position p at [s * kSW * Q * K + p]
+    int m;
     int *flag, *tinyf, *tseq, *p3n;
     LdsTanh ttab;
     LdsLog ltab;
@@ -168,17 +178,39 @@ template <int Q>
 __device__ __forceinline__ int sub_col(const SubCtx<Q> &c, int edge) {
     return *(const int *)((const char *)c.col_idx + ((uint32_t)edge << 2));
 }
+// column of this lane's slot i of row r (chunk rc), from the staged ring
+template <int Q>
+__device__ __forceinline__ int sub_lcol(const SubCtx<Q> &c, int r, const SubChunk &rc, int i) {
+    return c.cidx[(r % kCRing) * kSW * Q * SubCfg<Q>::K + min(c.j * rc.CS + i, rc.cnt - 1)];
+}
+// Staging of row q's indices into the ring: issue (one index per lane, lanes <
+// the chunk size) early, commit to LDS once the wavefront has waited on its
+// other loads anyway.
+template <int Q>
+__device__ __forceinline__ int sub_stage_issue(const SubCtx<Q> &c, int q) {
+    if (q >= c.m) return 0;
+    const SubChunk rc = sub_chunk(c.row_ptr, q, c.wave, Q);
+    const int L = threadIdx.x & 63;
+    return rc.cnt > 0 ? sub_col(c, rc.c0 + min(L, rc.cnt - 1)) : 0;
+}
+template <int Q>
+__device__ __forceinline__ void sub_stage_commit(const SubCtx<Q> &c, int q, int v) {
+    if (q >= c.m) return;
+    constexpr int W = Q * SubCfg<Q>::K;  // positions per wavefront chunk (40 / 64)
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    if ((int)(threadIdx.x & 63) < W) c.cidx[(q % kCRing) * kSW * W + (threadIdx.x & 63)] = (uint16_t)v;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
 
-// P1: t = tanh((L[col] - E_old)/2) for this lane's slots; returns whether
-// some lane's own edge has |t| <= 1e-10 (:159).
 // P1: t = tanh((L[col] - E_old)/2) for this lane's slots; returns whether
 // some lane's own edge has |t| <= 1e-10 (:159).  E_old is requested first
 // (independent of the column indices), then the indices, then the posterior
 // gather that needs them.
 template <int Q>
-__device__ __forceinline__ bool sub_p1(const SubCtx<Q> &c, const SubChunk &rc, double (&t)[SubCfg<Q>::K]) {
+__device__ __forceinline__ bool sub_p1(const SubCtx<Q> &c, int r, const SubChunk &rc, double (&t)[SubCfg<Q>::K]) {
     constexpr int K = SubCfg<Q>::K;
     bool tiny = false;
+    const int sv = sub_stage_issue(c, r + 1);  // row r+1's indices, committed below
     if (rc.cnt > 0) {
         const int nj = sub_nj(c, rc);
         int col[K];
@@ -186,9 +218,8 @@ __device__ __forceinline__ bool sub_p1(const SubCtx<Q> &c, const SubChunk &rc, d
 #pragma unroll
         for (int i = 0; i < K; ++i) {
             if (i < rc.CS) {
-                const int e = sub_edge(c, rc, i);
-                eo[i] = c.first ? 0.0 : ld_sub_msg(sub_e(c, e));
-                col[i] = sub_col(c, e);
+                eo[i] = c.first ? 0.0 : ld_sub_msg(sub_e(c, sub_edge(c, rc, i)));
+                col[i] = sub_lcol(c, r, rc, i);
             }
         }
         const char *Lsrc = c.first ? c.Cu : c.Lu;  // iteration 0: M = ch (:85-90); uniform
@@ -208,6 +239,7 @@ __device__ __forceinline__ bool sub_p1(const SubCtx<Q> &c, const SubChunk &rc, d
             }
         }
     }
+    sub_stage_commit(c, r + 1, sv);
     return __ballot(tiny) != 0ull;
 }
 
@@ -333,7 +365,7 @@ __device__ __forceinline__ void sub_p3_body(SubCtx<Q> &c, int r, double (&t)[Sub
     int col[K];
 #pragma unroll
     for (int i = 0; i < K; ++i)
-        if (i < rc.CS) col[i] = sub_col(c, sub_edge(c, rc, i));
+        if (i < rc.CS) col[i] = sub_lcol(c, r, rc, i);
     if (!tiny_row && div_nr_ok(P)) {  // the IEEE quotient without the scaling steps (cn_common.h)
 #pragma unroll
         for (int i = 0; i < K; ++i)
@@ -424,7 +456,7 @@ __device__ __forceinline__ void sub_body(SubCtx<Q> &c, int r, int m, double (&tc
                                          double (&toth)[SubCfg<Q>::K], bool &yoth) {
     if (r < m) sub_hop(c, r, tcur, ycur);
     if (r >= 1) sub_p3(c, r - 1, toth);
-    if (r + 1 < m) yoth = sub_p1(c, sub_chunk(c.row_ptr, r + 1, c.wave, Q), toth);
+    if (r + 1 < m) yoth = sub_p1(c, r + 1, sub_chunk(c.row_ptr, r + 1, c.wave, Q), toth);
 }
 
 template <int Q>
@@ -476,6 +508,8 @@ __global__ __launch_bounds__(64 * kSW, 1) void tile_sub_kernel(DevGraph g, DevSt
     c.dummy = (double *)(lds + ly.dummy) + f;
     c.slot = (double *)(lds + ly.slot) + f;
     c.ib = ib + f;
+    c.cidx = (uint16_t *)(lds + ly.cidx) + wave * Q * K;
+    c.m = g.m;
     c.flag = flags;
     c.tinyf = flags + kSR;
     c.tseq = flags + 2 * kSR;
@@ -498,7 +532,10 @@ __global__ __launch_bounds__(64 * kSW, 1) void tile_sub_kernel(DevGraph g, DevSt
         c.ep0 = it * m;
         double tA[K], tB[K];
         bool yA = false, yB = false;
-        if (m > 0) yA = sub_p1(c, sub_chunk(row_ptr, 0, wave, Q), tA);
+        if (m > 0) {
+            sub_stage_commit(c, 0, sub_stage_issue(c, 0));
+            yA = sub_p1(c, 0, sub_chunk(row_ptr, 0, wave, Q), tA);
+        }
         for (int r = 0; r <= m; r += 2) {
             sub_body(c, r, m, tA, yA, tB, yB);
             if (r + 1 <= m) sub_body(c, r + 1, m, tB, yB, tA, yA);
@@ -577,7 +614,8 @@ __global__ __launch_bounds__(64 * kSW, 1) void tile_sub_kernel(DevGraph g, DevSt
 template <int Q>
 size_t sub_lds_bytes_q(const DevGraph &g) {
     constexpr int F = SubCfg<Q>::F, K = SubCfg<Q>::K;
-    if (!g.std_form || !g.a_packed || g.k <= 0 || g.max_row_deg > kSW * Q * K) return 0;
+    if (!g.std_form || !g.a_packed || g.k <= 0 || g.max_row_deg > kSW * Q * K || Q * K > 64 || g.n > 65535)
+        return 0;
     const size_t b = sub_layout(g.k, g.m, F).total;
     return b <= kSubLdsMax ? b : 0;
 }
