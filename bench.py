@@ -347,10 +347,18 @@ def main():
     elapsed = max_over_ranks(dist, elapsed, local)
 
     # extra SNR points (one step each, after the headline's timed region), on
-    # the streaming schedule: there frames stop at very different iterations
+    # the streaming schedule: there frames stop at very different iterations,
+    # so the step streams its frames through a quarter as many slots (a fresh,
+    # smaller workspace) and a slot is refilled as soon as its frame stops
     snr_points = []
     extra_sched = "stream"
-    for i, x in enumerate(v for v in args.extra_snr.split(",") if v.strip()):
+    extra = [v for v in args.extra_snr.split(",") if v.strip()]
+    extra_slots = None
+    if extra and pgraph is None:
+        dec.close()
+        extra_slots = max(64, (B // 4) // 64 * 64)
+        dec = Decoder(graph, extra_slots)
+    for i, x in enumerate(extra):
         x = float(x)
         sg = 1.0 / math.sqrt(2.0 * 1.0 * (10.0 ** (x * 0.1)))
         barrier(dist, local)
@@ -360,7 +368,7 @@ def main():
         dt = max_over_ranks(dist, time.perf_counter() - t1, local)
         f = int(c[0, 0])
         snr_points.append({"snr_db": x, "value": f / dt, "unit": "codewords/s", "info_bits_per_s": f * k / dt,
-                           "ms": dt * 1e3, "frames": f, "schedule": extra_sched,
+                           "ms": dt * 1e3, "frames": f, "schedule": extra_sched, "slots": extra_slots,
                            "avg_iters": int(c[0, 6]) / max(f, 1),
                            "fer": int(c[0, 1]) / max(f, 1), "ber": int(c[0, 2]) / (k * max(f, 1))})
 

@@ -90,6 +90,9 @@ hipError_t launch_tile_stream(const DevGraph &g, const DevState &st, int max_ite
 int sub_frames(const DevGraph &g);
 size_t sub_lds_bytes(const DevGraph &g);
 hipError_t launch_tile_sub(const DevGraph &g, const DevState &st, int max_iter, bool nllr, hipStream_t s);
+hipError_t launch_tile_sub_stream(const DevGraph &g, const DevState &st, int max_iter, bool nllr, uint64_t seed,
+                                  int snr_point, double sigma, int64_t frame0, int64_t total,
+                                  unsigned long long *next, unsigned long long *ctr, hipStream_t s);
 hipError_t launch_stream_init(const DevGraph &g, const DevState &st, hipStream_t s);
 hipError_t launch_refill(const DevGraph &g, const DevState &st, uint64_t seed, int snr_point, double sigma,
                          int64_t frame0, int64_t total, unsigned long long *next, hipStream_t s);

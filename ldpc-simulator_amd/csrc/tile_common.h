@@ -24,13 +24,19 @@ __device__ __forceinline__ void lds_st(int *p, int v) {
 // waiting for its outstanding global stores.
 __device__ __forceinline__ void lds_release() { __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local"); }
 __device__ __forceinline__ void lds_acquire() { __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local"); }
-// Polls sleep (s_sleep 1) between flag reads.
+// Polls sleep (s_sleep LDPC_POLL_SLEEP) between flag reads.
+#ifndef LDPC_POLL_SLEEP
+#define LDPC_POLL_SLEEP 1
+#endif
+__device__ __forceinline__ void poll_pause() {
+    if (LDPC_POLL_SLEEP > 0) __builtin_amdgcn_s_sleep(LDPC_POLL_SLEEP);
+}
 __device__ __forceinline__ void wait_flag(const int *p, int v) {
-    while (uniform(lds_ld(p)) != v) __builtin_amdgcn_s_sleep(1);
+    while (uniform(lds_ld(p)) != v) poll_pause();
     lds_acquire();
 }
 __device__ __forceinline__ void wait_ge(const int *p, int v) {
-    while (uniform(lds_ld(p)) < v) __builtin_amdgcn_s_sleep(1);
+    while (uniform(lds_ld(p)) < v) poll_pause();
     lds_acquire();
 }
 // Load through L2 (not this CU's L1): data another wavefront of the workgroup

@@ -710,17 +710,25 @@ bool use_tile(const DevGraph &g) {
     return force != 0 && tile_lds_bytes(g) > 0;
 }
 
+// Streaming Monte-Carlo in one persistent launch per SNR point: tile_stream_kernel
+// (64 frames per workgroup) or tile_sub_stream_kernel (16-frame sub-tiles,
+// wimax_2304_0.5).  LDPC_TILE_STREAM=0 falls back to the separate launches.
+static bool sub16(const DevGraph &g) { return sub_enabled(g) && sub_frames(g) == 16; }
 bool use_tile_stream(const DevGraph &g) {
     const char *e = getenv("LDPC_TILE_STREAM");
+    if (e && atoi(e) == 0) return false;
     const size_t lds = tile64_lds_bytes(g);
     // + the kernel's static per-lane state (itl, freshl: 2 x 64 ints)
-    return (!e || atoi(e) != 0) && lds > 0 && lds + 2 * kTile * sizeof(int) <= kTileLdsMax;
+    if (lds) return lds + 2 * kTile * sizeof(int) <= kTileLdsMax;
+    return sub16(g);
 }
 
 hipError_t launch_tile_stream(const DevGraph &g, const DevState &st, int max_iter, bool nllr, uint64_t seed,
                               int snr_point, double sigma, int64_t frame0, int64_t total, unsigned long long *next,
                               unsigned long long *ctr, hipStream_t s) {
     const size_t lds = tile64_lds_bytes(g);
+    if (!lds && sub16(g))
+        return launch_tile_sub_stream(g, st, max_iter, nllr, seed, snr_point, sigma, frame0, total, next, ctr, s);
     if (!lds || !g.a_packed || !st.ubits || st.ntiles > st.nslots) return hipErrorInvalidValue;
     tile_stream_kernel<<<st.ntiles, 64 * kTW, lds, s>>>(g, st, max_iter, nllr ? 1 : 0, g.col_idx, g.row_ptr,
                                                         kAtanhCoef, seed, snr_point, sigma, frame0, total, next, ctr);

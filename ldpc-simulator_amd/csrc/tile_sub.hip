@@ -41,6 +41,7 @@
 #include <cstdlib>
 
 #include "cn_common.h"
+#include "frame_source.h"
 #include "spa_device.h"
 #include "spa_math.h"
 #include "tile_common.h"
@@ -65,6 +66,9 @@ struct SubCfg {
 // P3(r-1); the S additions of a row wait on the per-row P3 completion counts,
 // and the chain slots are reused every 4 rows.
 constexpr int kSR = 4;  // chain slots
+#ifndef LDPC_SUB_HOPPRIO
+#define LDPC_SUB_HOPPRIO 2
+#endif
 __device__ __forceinline__ double ld_sub_msg(const double *p) { return __builtin_nontemporal_load(p); }
 __device__ __forceinline__ void st_sub_msg(double *p, double v) { __builtin_nontemporal_store(v, p); }
 
@@ -144,6 +148,7 @@ struct SubCtx {
     int k, wave, j, f;
     int ep0;
     bool first, live;
+    bool fresh;  // streaming: this lane's frame is on its first pass (M = L - 0, L = ch)
     int ntiny;
 };
 
@@ -218,7 +223,7 @@ __device__ __forceinline__ bool sub_p1(const SubCtx<Q> &c, int r, const SubChunk
 #pragma unroll
         for (int i = 0; i < K; ++i) {
             if (i < rc.CS) {
-                eo[i] = c.first ? 0.0 : ld_sub_msg(sub_e(c, sub_edge(c, rc, i)));
+                eo[i] = (c.first || c.fresh) ? 0.0 : ld_sub_msg(sub_e(c, sub_edge(c, rc, i)));
                 col[i] = sub_lcol(c, r, rc, i);
             }
         }
@@ -311,7 +316,7 @@ __device__ __forceinline__ void sub_hop(const SubCtx<Q> &c, int r, const double 
         wait_flag(c.flag + s, ep + c.wave);
         P = *sl;
     }
-    __builtin_amdgcn_s_setprio(2);
+    __builtin_amdgcn_s_setprio(LDPC_SUB_HOPPRIO);
     int last = -1;
 #pragma unroll
     for (int jj = 0; jj < Q; ++jj) {
@@ -522,6 +527,7 @@ __global__ __launch_bounds__(64 * kSW, 1) void tile_sub_kernel(DevGraph g, DevSt
     c.j = j;
     c.f = f;
     c.ntiny = 0;
+    c.fresh = false;
     const int m = g.m;
     const int nthr = kSW * Q;       // (wavefront, lane group) pairs
     const int me = wave * Q + j;    // this lane's pair
@@ -611,6 +617,199 @@ __global__ __launch_bounds__(64 * kSW, 1) void tile_sub_kernel(DevGraph g, DevSt
     }
 }
 
+// Streaming Monte-Carlo on sub-tiles (tile_kernels.hip's tile_stream_kernel,
+// at 16 frames per workgroup): every frame slot f is at its own iteration;
+// after each pass a slot whose frame stopped adds that frame's counters
+// (count_kernel's definitions, main.py:130-138) and takes the next frame
+// index from one device counter; the frame is generated in place (gen_lane:
+// ch and L = ch, so its next pass forms M = L - 0, its iteration 0).  Each
+// frame decodes exactly as in the static schedule, so the counters are
+// identical.  A workgroup exits once the supply is out and its slots drained.
+template <int Q>
+__global__ __launch_bounds__(64 * kSW, 1) void tile_sub_stream_kernel(
+    DevGraph g, DevState st, int max_iter, int nllr, const int *__restrict__ col_idx,
+    const int *__restrict__ row_ptr, AtanhCoef ac, uint64_t seed, int snr_point, double sigma, int64_t frame0,
+    int64_t total, unsigned long long *next, unsigned long long *ctr) {
+    constexpr int F = SubCfg<Q>::F, K = SubCfg<Q>::K;
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+    __shared__ int itl[F], freshl[F];
+    const SubLayout ly = sub_layout(g.k, g.m, F);
+    double *S = (double *)(lds + ly.S);
+    MathLds &mlds = *(MathLds *)(lds + ly.math);
+    uint32_t *zb = (uint32_t *)(lds + ly.zb);
+    uint32_t *ib = (uint32_t *)(lds + ly.ib);
+    int *bad = (int *)(lds + ly.lane_i);
+    int *cntl = bad + F;
+    int *livel = cntl + F;
+    int *flags = (int *)(lds + ly.flags);
+    const int kw = (g.k + 31) >> 5, mw = (g.m + 31) >> 5;
+    const int tile = blockIdx.x / Q, sub = blockIdx.x % Q;
+    if (tile >= st.ntiles) return;  // block-uniform
+
+    fill_math_lds(mlds);
+    for (int i = threadIdx.x; i < g.k * F; i += blockDim.x) S[i] = 0.0;
+    for (int i = threadIdx.x; i < (kw + mw) * F; i += blockDim.x) zb[i] = 0u;
+    for (int i = threadIdx.x; i < 2 * F; i += blockDim.x) bad[i] = 0;
+    if (threadIdx.x < 2 * kSR) flags[threadIdx.x] = -1;
+    if (threadIdx.x >= 2 * kSR && threadIdx.x < 2 * kSR + 6) flags[threadIdx.x] = 0;
+    const int lane = threadIdx.x & 63;
+    const int wave = uniform(threadIdx.x >> 6);
+    const int j = lane / F, f = lane % F;
+    const int lane64 = sub * F + f;
+    const bool slot_lane = wave == 0 && j == 0;  // the lane that owns frame slot f
+    bool want = slot_lane;
+    if (slot_lane) {
+        livel[f] = 0;
+        itl[f] = 0;
+        freshl[f] = 0;
+    }
+
+    SubCtx<Q> c;
+    c.col_idx = col_idx;
+    c.row_ptr = row_ptr;
+    const size_t lo = (size_t)lane64;
+    c.Eb = st.E + (size_t)tile * g.nnz * kTile + lo;
+    c.Lb = st.L + (size_t)tile * g.n * kTile + lo;
+    c.Cb = st.ch + (size_t)tile * g.n * kTile + lo;
+    c.Eu = (const char *)(st.E + (size_t)tile * g.nnz * kTile);
+    c.Lu = (const char *)(st.L + (size_t)tile * g.n * kTile);
+    c.Cu = (const char *)(st.ch + (size_t)tile * g.n * kTile);
+    c.lo8 = (uint32_t)lo * 8u;
+    c.Tb = st.T + (size_t)blockIdx.x * g.max_row_deg * F + f;
+    c.S = S + f;
+    c.dummy = (double *)(lds + ly.dummy) + f;
+    c.slot = (double *)(lds + ly.slot) + f;
+    c.ib = ib + f;
+    c.cidx = (uint16_t *)(lds + ly.cidx) + wave * Q * K;
+    c.m = g.m;
+    c.flag = flags;
+    c.tinyf = flags + kSR;
+    c.tseq = flags + 2 * kSR;
+    c.p3n = flags + 2 * kSR + 2;
+    c.ttab = LdsTanh{mlds.tanh};
+    c.ltab = LdsLog{mlds.log};
+    c.ac = ac;
+    c.k = g.k;
+    c.wave = wave;
+    c.j = j;
+    c.f = f;
+    c.ntiny = 0;
+    c.first = false;
+    const int m = g.m;
+    const int nthr = kSW * Q;
+    const int me = wave * Q + j;
+    uint32_t *ul = st.ubits + (size_t)tile * kw * kTile;  // u-bit stage: the slots' own ubits words
+    const uint32_t *Ut = st.ubits + (size_t)tile * kw * kTile + lane64;
+
+    for (int pass = 0;; ++pass) {
+        if (wave == 0) {  // refill: slots without a frame take the next indices and generate them
+            const unsigned long long w = __ballot(want);
+            if (w != 0ull) {
+                const int first = __ffsll((long long)w) - 1;
+                unsigned long long base = 0ull;
+                if (lane == first) base = atomicAdd(next, (unsigned long long)__popcll(w));
+                base = __shfl(base, first);
+                const unsigned long long below = lane ? (w & (~0ull >> (64 - lane))) : 0ull;
+                const int64_t idx = (int64_t)(base + (unsigned long long)__popcll(below));
+                const bool have = want && idx < total;
+                if (have) gen_lane(g, st, tile, lane64, frame0 + idx, seed, snr_point, sigma, g.a_packed, ul, true, true);
+                if (want) {
+                    livel[f] = have ? 1 : 0;
+                    freshl[f] = have ? 1 : 0;
+                    itl[f] = 0;
+                }
+            }
+            want = false;
+            const unsigned long long any = __ballot(slot_lane && livel[f] != 0);
+            if (lane == 0) flags[2 * kSR + 1] = any != 0ull ? 1 : 0;
+        }
+        __syncthreads();
+        if (!flags[2 * kSR + 1]) break;  // supply exhausted, every slot drained
+        c.live = livel[f] != 0;
+        c.fresh = freshl[f] != 0;
+        c.ep0 = pass * m;
+        double tA[K], tB[K];
+        bool yA = false, yB = false;
+        if (m > 0) {
+            sub_stage_commit(c, 0, sub_stage_issue(c, 0));
+            yA = sub_p1(c, 0, sub_chunk(row_ptr, 0, wave, Q), tA);
+        }
+        for (int r = 0; r <= m; r += 2) {
+            sub_body(c, r, m, tA, yA, tB, yB);
+            if (r + 1 <= m) sub_body(c, r + 1, m, tB, yB, tA, yA);
+        }
+        __syncthreads();
+
+        int my_cnt = 0;
+        for (int col = me; col < g.k; col += nthr) {
+            double *sp = c.S + (size_t)col * F;
+            const double Sj = *sp;
+            *sp = 0.0;
+            const double chj = c.Cb[(size_t)col * kTile];
+            const double Lj = chj + Sj;  // channel added after the sum (:173,185)
+            if (nllr) {
+                const double ap = ld_l2(c.Lb + (size_t)col * kTile);  // previous L (= ch on a frame's first pass)
+                my_cnt += (fabs(Lj) <= 7.0 && ap * Lj < 0.0) ? 1 : 0;
+            }
+            if (c.live) c.Lb[(size_t)col * kTile] = Lj;
+            if (!(Lj < 0.0)) atomicOr(zb + (col >> 5) * F + f, 1u << (col & 31));
+        }
+        if (nllr && my_cnt) atomicAdd(cntl + f, my_cnt);
+        __syncthreads();
+
+        uint32_t acc = 0u;  // syndrome (:191-204)
+        for (int r = me; r < m; r += nthr) {
+            const uint32_t *ar = g.a_packed + (size_t)r * kw;
+            uint32_t par = ib[(r >> 5) * F + f] >> (r & 31);
+            for (int w = 0; w < kw; ++w) par += __builtin_popcount(ar[w] & zb[w * F + f]);
+            acc |= par & 1u;
+        }
+        if (acc) atomicOr((uint32_t *)bad + f, 1u);
+        __syncthreads();
+
+        if (wave == 0) {  // per-slot exits and counters (vn_kernel's stream variant)
+            unsigned long long cv[7] = {0, 0, 0, 0, 0, 0, 0};
+            bool fin = false;
+            if (slot_lane && c.live) {
+                const int it = itl[f];
+                const bool ok = bad[f] == 0;  // Result.OK at this iteration (:231-241)
+                fin = ok || it == max_iter - 1;  // else DATA_TRANSFER_NOT_OK (:244-253)
+                if (fin) {
+                    int err = 0;
+                    if (!ok)  // main.py:130-138: u vs z^1 of a failed frame
+                        for (int w = 0; w < kw; ++w) err += __builtin_popcount(Ut[w * kTile] ^ zb[w * F + f]);
+                    cv[0] = 1;
+                    cv[1] = ok ? 0 : 1;
+                    cv[2] = (unsigned long long)err;
+                    cv[3] = ok ? (unsigned long long)it : 0;
+                    cv[4] = ok ? 1 : 0;
+                    cv[5] = nllr ? (unsigned long long)cntl[f] : 0;
+                    cv[6] = (unsigned long long)(it + 1);
+                    livel[f] = 0;
+                    want = true;
+                } else {
+                    itl[f] = it + 1;
+                }
+                freshl[f] = 0;
+            }
+            if (__ballot(fin) != 0ull) {
+#pragma unroll
+                for (int i = 0; i < 7; ++i) {
+                    const unsigned long long sm = wave_sum(cv[i]);
+                    if (lane == 0 && sm) atomicAdd(&ctr[i], sm);
+                }
+            }
+            if (slot_lane) {
+                bad[f] = 0;
+                cntl[f] = 0;
+            }
+        }
+        __syncthreads();  // wave 0 has read zb (error bits) before it is cleared
+        for (int i = threadIdx.x; i < (kw + mw) * F; i += blockDim.x) zb[i] = 0u;
+        __syncthreads();
+    }
+}
+
 template <int Q>
 size_t sub_lds_bytes_q(const DevGraph &g) {
     constexpr int F = SubCfg<Q>::F, K = SubCfg<Q>::K;
@@ -632,6 +831,19 @@ int sub_frames(const DevGraph &g) {
 size_t sub_lds_bytes(const DevGraph &g) {
     const int F = sub_frames(g);
     return F == 16 ? sub_lds_bytes_q<4>(g) : F == 8 ? sub_lds_bytes_q<8>(g) : 0;
+}
+
+hipError_t launch_tile_sub_stream(const DevGraph &g, const DevState &st, int max_iter, bool nllr, uint64_t seed,
+                                  int snr_point, double sigma, int64_t frame0, int64_t total,
+                                  unsigned long long *next, unsigned long long *ctr, hipStream_t s) {
+    const size_t lds = sub_lds_bytes_q<4>(g);
+    // the 16-frame form only (+ 2 x 16 ints of static LDS per-slot state)
+    if (!lds || !g.a_packed || !st.ubits || st.ntiles > st.nslots || lds + 2 * 16 * sizeof(int) > kSubLdsMax)
+        return hipErrorInvalidValue;
+    tile_sub_stream_kernel<4><<<st.ntiles * 4, 64 * kSW, lds, s>>>(g, st, max_iter, nllr ? 1 : 0, g.col_idx, g.row_ptr,
+                                                                   kAtanhCoef, seed, snr_point, sigma, frame0, total,
+                                                                   next, ctr);
+    return hipGetLastError();
 }
 
 hipError_t launch_tile_sub(const DevGraph &g, const DevState &st, int max_iter, bool nllr, hipStream_t s) {

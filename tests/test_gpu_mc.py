@@ -142,6 +142,8 @@ def test_stream_zero_frames(gpu_available):
     ("BCH_7_4_1_strip", 64, 5000, 10, (0.0, 4.0)),
     ("wimax_576_0.5", 128, 130, 1, (1.0, 6.0)),     # max_iter 1: every frame stops after its first pass
     ("wimax_576_0.5", 4096, 70, 8, (0.5,)),         # far fewer frames than slots (idle workgroups)
+    ("wimax_2304_0.5", 256, 700, 12, (1.0, 3.0)),   # 16-frame sub-tiles (tile_sub_stream_kernel)
+    ("wimax_2304_0.5", 64, 150, 1, (2.0,)),         # sub-tiles, max_iter 1
 ])
 def test_tile_stream_equals_split_stream(gpu_available, code, cap, frames, T, snrs):
     dec = _decoder(code, cap)
@@ -163,9 +165,9 @@ def test_stream_tail_compaction_keeps_counters(gpu_available, monkeypatch):
     code, cap, frames, T = "wimax_2304_0.5", 256, 1500, 20
     dec = _decoder(code, cap)
     sig = [oracle.sigma_for_snr(s) for s in (2.5, 3.0)]
-    a = dec.mc_run(SEED, sig, frames, 11, T, nllr=True)
+    a = dec.mc_run(SEED, sig, frames, 11, T, nllr=True, split=True)
     monkeypatch.setenv("LDPC_COMPACT", "0")
-    b = dec.mc_run(SEED, sig, frames, 11, T, nllr=True)
+    b = dec.mc_run(SEED, sig, frames, 11, T, nllr=True, split=True)
     monkeypatch.delenv("LDPC_COMPACT")
     c = dec.mc_run(SEED, sig, frames, 11, T, nllr=True, static=True)
     np.testing.assert_array_equal(a, b)
