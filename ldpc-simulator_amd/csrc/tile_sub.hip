@@ -66,9 +66,6 @@ struct SubCfg {
 // P3(r-1); the S additions of a row wait on the per-row P3 completion counts,
 // and the chain slots are reused every 4 rows.
 constexpr int kSR = 4;  // chain slots
-#ifndef LDPC_SUB_HOPPRIO
-#define LDPC_SUB_HOPPRIO 2
-#endif
 __device__ __forceinline__ double ld_sub_msg(const double *p) { return __builtin_nontemporal_load(p); }
 __device__ __forceinline__ void st_sub_msg(double *p, double v) { __builtin_nontemporal_store(v, p); }
 
@@ -313,10 +310,10 @@ __device__ __forceinline__ void sub_hop(const SubCtx<Q> &c, int r, const double 
     double *sl = c.slot + s * F;
     double P = 1.0;  // 1.0 * t0 == t0 exactly
     if (c.wave != 0) {
-        wait_flag(c.flag + s, ep + c.wave);
+        wait_flag<false>(c.flag + s, ep + c.wave);
         P = *sl;
     }
-    __builtin_amdgcn_s_setprio(LDPC_SUB_HOPPRIO);
+    __builtin_amdgcn_s_setprio(2);
     int last = -1;
 #pragma unroll
     for (int jj = 0; jj < Q; ++jj) {
@@ -354,14 +351,14 @@ __device__ __forceinline__ void sub_p3_body(SubCtx<Q> &c, int r, double (&t)[Sub
     if (rc.deg == 0) return;
     const int s = r & (kSR - 1);
     const int ep = ((c.ep0 + r) & 0x3ffffff) * 32;
-    wait_flag(c.flag + s, ep + kSW);
+    wait_flag<false>(c.flag + s, ep + kSW);
     const bool tiny_row = uniform(lds_ld(c.tinyf + s)) != 0;
     if (rc.cnt == 0) {  // no edges here (short rows): still take part in a rare row's parking count
         if (tiny_row) {
             c.ntiny += 1;
             if ((threadIdx.x & 63) == 0)
                 __hip_atomic_fetch_add(c.tseq, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-            wait_flag(c.tseq, c.ntiny * kSW);
+            wait_flag<false>(c.tseq, c.ntiny * kSW);
         }
         return;
     }
@@ -389,7 +386,7 @@ __device__ __forceinline__ void sub_p3_body(SubCtx<Q> &c, int r, double (&t)[Sub
         __builtin_amdgcn_s_waitcnt(0);  // scratch stores have reached L2
         c.ntiny += 1;
         if ((threadIdx.x & 63) == 0) __hip_atomic_fetch_add(c.tseq, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-        wait_flag(c.tseq, c.ntiny * kSW);
+        wait_flag<false>(c.tseq, c.ntiny * kSW);
 #pragma unroll
         for (int i = 0; i < K; ++i) {
             if (i < rc.CS) {
@@ -449,7 +446,7 @@ __device__ __forceinline__ void sub_p3_body(SubCtx<Q> &c, int r, double (&t)[Sub
 template <int Q>
 __device__ __forceinline__ void sub_p3(SubCtx<Q> &c, int r, double (&t)[SubCfg<Q>::K]) {
     const int g = c.ep0 + r;
-    if (g > 0) wait_ge(c.p3n + ((g - 1) & 3), kSW * (((g - 1) >> 2) + 1));
+    if (g > 0) wait_ge<false>(c.p3n + ((g - 1) & 3), kSW * (((g - 1) >> 2) + 1));
     sub_p3_body(c, r, t);
     lds_release();  // this row's S additions before the count
     if ((threadIdx.x & 63) == 0)
