@@ -59,6 +59,45 @@ __host__ __device__ __forceinline__ double np_tanh(double x, const Tab &tab) {
     return dfrom(dbits(r) | (ux & 0x8000000000000000ull));
 }
 
+// np_tanh of G independent arguments, Horner steps in lockstep across them:
+// each argument gets exactly np_tanh's operations in np_tanh's order (so the
+// results are bit-identical), but the G coefficient-table reads of a step are
+// independent and can be in flight together instead of one dependent read per
+// step of one chain.
+template <int G, class Tab>
+__host__ __device__ __forceinline__ void np_tanh_n(double (&x)[G], const Tab &tab) {
+    int idx[G];
+    double y[G], r[G], b0[G];
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+        const uint64_t nd = dbits(x[g]) & 0x7ff8000000000000ull;
+        int hi = (int)(nd >> 32) - 0x3fc00000;
+        hi = hi < 0 ? 0 : (hi > 0x780000 ? 0x780000 : hi);
+        idx[g] = hi >> 19;
+        const Pair p0 = tab(0, idx[g]);
+        y[g] = __builtin_fabs(x[g]) - p0.a;
+        b0[g] = p0.b;
+        const Pair c = tab(8, idx[g]);
+        r[g] = __builtin_fma(c.b, y[g], c.a);  // c16*y + c15
+    }
+#pragma unroll
+    for (int p = 7; p >= 1; --p) {
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+            const Pair c = tab(p, idx[g]);
+            r[g] = __builtin_fma(r[g], y[g], c.b);
+            r[g] = __builtin_fma(r[g], y[g], c.a);
+        }
+    }
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+        const uint64_t ux = dbits(x[g]);
+        double v = __builtin_fma(r[g], y[g], b0[g]);
+        if ((ux & 0x7ff8000000000000ull) > 0x7fe0000000000000ull) v = 1.0;
+        x[g] = dfrom(dbits(v) | (ux & 0x8000000000000000ull));
+    }
+}
+
 // ----------------------------------------------------------------- log
 constexpr double kLn2Hi = 0x1.62e42fefa3800p-1;  // 11 trailing zero bits: k*kLn2Hi exact
 constexpr double kLn2Lo = 0x1.ef35793c76730p-45;

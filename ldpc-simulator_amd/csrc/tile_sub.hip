@@ -66,6 +66,11 @@ struct SubCfg {
 // P3(r-1); the S additions of a row wait on the per-row P3 completion counts,
 // and the chain slots are reused every 4 rows.
 constexpr int kSR = 4;  // chain slots
+// P1: slots per lockstep tanh group (np_tanh_n).  1 is fastest: groups of 2
+// and 3 overlap their table reads but spill (+8 % / 4x time), and the
+// straight-line form of a single slot alone measured 2 % faster than np_tanh
+// behind a per-slot branch (profiles r2u/r2v logs).
+constexpr int kSG = 1;
 __device__ __forceinline__ double ld_sub_msg(const double *p) { return __builtin_nontemporal_load(p); }
 __device__ __forceinline__ void st_sub_msg(double *p, double v) { __builtin_nontemporal_store(v, p); }
 
@@ -219,7 +224,7 @@ __device__ __forceinline__ bool sub_p1(const SubCtx<Q> &c, int r, const SubChunk
         double eo[K];
 #pragma unroll
         for (int i = 0; i < K; ++i) {
-            if (i < rc.CS) {
+            if (i - i % kSG < rc.CS) {  // every slot of a group that runs
                 eo[i] = (c.first || c.fresh) ? 0.0 : ld_sub_msg(sub_e(c, sub_edge(c, rc, i)));
                 col[i] = sub_lcol(c, r, rc, i);
             }
@@ -227,17 +232,35 @@ __device__ __forceinline__ bool sub_p1(const SubCtx<Q> &c, int r, const SubChunk
         const char *Lsrc = c.first ? c.Cu : c.Lu;  // iteration 0: M = ch (:85-90); uniform
 #pragma unroll
         for (int i = 0; i < K; ++i)
-            if (i < rc.CS) t[i] = ld_l2((const double *)(Lsrc + sub_off(c, col[i])));
+            if (i - i % kSG < rc.CS) t[i] = ld_l2((const double *)(Lsrc + sub_off(c, col[i])));
+        // tanh in groups of kSG slots evaluated in lockstep (np_tanh_n: the
+        // groups' table reads overlap); a group runs if its first slot is in
+        // the chunk (slots past CS hold clamped, valid data and end as 1.0)
 #pragma unroll
-        for (int i = 0; i < K; ++i) {
-            if (i < rc.CS) {
-                const double M = c.first ? t[i] : t[i] - eo[i];  // :85-90 / :260-268
-                const double d = M * 0.5;
-                const double r = np_tanh(d, c.ttab);
-                t[i] = d > 17.5 ? kCL : (d < -17.5 ? -kCL : r);  // :138-146
-                tiny |= i < nj && !(fabs(t[i]) > kTiny);
-                // slots past this lane's piece: 1.0, an exact no-op in the chain product
-                if (i >= nj) t[i] = 1.0;
+        for (int g0 = 0; g0 < K; g0 += kSG) {
+            if (g0 < rc.CS) {
+                constexpr int G0 = kSG;
+                double d[G0];
+#pragma unroll
+                for (int q = 0; q < G0; ++q) {
+                    const int i = g0 + q < K ? g0 + q : K - 1;
+                    const double M = c.first ? t[i] : t[i] - eo[i];  // :85-90 / :260-268
+                    d[q] = M * 0.5;
+                }
+                double th[G0];
+#pragma unroll
+                for (int q = 0; q < G0; ++q) th[q] = d[q];
+                np_tanh_n<G0>(th, c.ttab);
+#pragma unroll
+                for (int q = 0; q < G0; ++q) {
+                    const int i = g0 + q;
+                    if (i < K) {
+                        const double tv = d[q] > 17.5 ? kCL : (d[q] < -17.5 ? -kCL : th[q]);  // :138-146
+                        tiny |= i < nj && !(fabs(tv) > kTiny);
+                        // slots past this lane's piece: 1.0, an exact no-op in the chain product
+                        t[i] = i < nj ? tv : 1.0;
+                    }
+                }
             }
         }
     }
