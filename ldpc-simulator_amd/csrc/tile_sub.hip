@@ -71,6 +71,13 @@ constexpr int kSR = 4;  // chain slots
 // straight-line form of a single slot alone measured 2 % faster than np_tanh
 // behind a per-slot branch (profiles r2u/r2v logs).
 constexpr int kSG = 1;
+// P1 loads and evaluates tanh for all K slots of a lane, branch-free: slots
+// past the chunk's CS hold clamped, valid data (their t ends as 1.0 and is never
+// used), and the straight-line code lets each slot's math wait only for its own
+// loads (+2.7 % over a per-slot branch, profiles r2x logs; the same for P3's
+// E_new math measured neutral).  P3's column-sum additions run as all reads,
+// all adds, all writes: one LDS round trip per row instead of one per slot (a
+// lane's slots never share a column within a row; +1.1 %, profiles r2z logs).
 __device__ __forceinline__ double ld_sub_msg(const double *p) { return __builtin_nontemporal_load(p); }
 __device__ __forceinline__ void st_sub_msg(double *p, double v) { __builtin_nontemporal_store(v, p); }
 
@@ -224,7 +231,7 @@ __device__ __forceinline__ bool sub_p1(const SubCtx<Q> &c, int r, const SubChunk
         double eo[K];
 #pragma unroll
         for (int i = 0; i < K; ++i) {
-            if (i - i % kSG < rc.CS) {  // every slot of a group that runs
+            {
                 eo[i] = (c.first || c.fresh) ? 0.0 : ld_sub_msg(sub_e(c, sub_edge(c, rc, i)));
                 col[i] = sub_lcol(c, r, rc, i);
             }
@@ -232,13 +239,13 @@ __device__ __forceinline__ bool sub_p1(const SubCtx<Q> &c, int r, const SubChunk
         const char *Lsrc = c.first ? c.Cu : c.Lu;  // iteration 0: M = ch (:85-90); uniform
 #pragma unroll
         for (int i = 0; i < K; ++i)
-            if (i - i % kSG < rc.CS) t[i] = ld_l2((const double *)(Lsrc + sub_off(c, col[i])));
+            t[i] = ld_l2((const double *)(Lsrc + sub_off(c, col[i])));
         // tanh in groups of kSG slots evaluated in lockstep (np_tanh_n: the
         // groups' table reads overlap); a group runs if its first slot is in
         // the chunk (slots past CS hold clamped, valid data and end as 1.0)
 #pragma unroll
         for (int g0 = 0; g0 < K; g0 += kSG) {
-            if (g0 < rc.CS) {
+            {
                 constexpr int G0 = kSG;
                 double d[G0];
 #pragma unroll
@@ -389,8 +396,7 @@ __device__ __forceinline__ void sub_p3_body(SubCtx<Q> &c, int r, double (&t)[Sub
     const int nj = sub_nj(c, rc);
     int col[K];
 #pragma unroll
-    for (int i = 0; i < K; ++i)
-        if (i < rc.CS) col[i] = sub_lcol(c, r, rc, i);
+    for (int i = 0; i < K; ++i) col[i] = sub_lcol(c, r, rc, i);  // clamped position: valid for every slot
     if (!tiny_row && div_nr_ok(P)) {  // the IEEE quotient without the scaling steps (cn_common.h)
 #pragma unroll
         for (int i = 0; i < K; ++i)
@@ -441,19 +447,24 @@ __device__ __forceinline__ void sub_p3_body(SubCtx<Q> &c, int r, double (&t)[Sub
     // lanes of a row share (col, frame)); the identity edge goes to `dummy`
     double EnI = 0.0;
     int colI = -1;
+    double *sp[K];
+    double sv[K];
 #pragma unroll
     for (int i = 0; i < K; ++i) {
-        if (i < rc.CS) {
-            const bool own = i < nj;
-            const bool a = own && col[i] < c.k;
-            double *sp = a ? c.S + (size_t)col[i] * F : c.dummy;
-            *sp = *sp + t[i];
-            if (own && !a) {
-                EnI = t[i];
-                colI = col[i];
-            }
+        const bool own = i < nj;  // nj <= CS
+        const bool a = own && col[i] < c.k;
+        sp[i] = a ? c.S + (size_t)col[i] * F : c.dummy;
+        if (own && !a) {
+            EnI = t[i];
+            colI = col[i];
         }
     }
+#pragma unroll
+    for (int i = 0; i < K; ++i) sv[i] = *sp[i];
+#pragma unroll
+    for (int i = 0; i < K; ++i) sv[i] = sv[i] + t[i];
+#pragma unroll
+    for (int i = 0; i < K; ++i) *sp[i] = sv[i];
     if (colI >= 0) {  // identity column: L = ch + (0 + E) (:173-185)
         const double Lj = *sub_c(c, colI) + (0.0 + EnI);
         if (c.live) *sub_l(c, colI) = Lj;
