@@ -78,6 +78,12 @@ constexpr int kSG = 1;
 // E_new math measured neutral).  P3's column-sum additions run as all reads,
 // all adds, all writes: one LDS round trip per row instead of one per slot (a
 // lane's slots never share a column within a row; +1.1 %, profiles r2z logs).
+// Template flag BF selects these forms per kernel: bit 0 the branch-free P1,
+// bit 1 the branch-free P3 (clamped column reads, batched S updates).  The
+// streaming kernel (more live refill state, more spills) gains from bit 0
+// (+3.4 % at 2 dB) but loses 8 % to bit 1 (profiles/r2ag_stream_bf).
+constexpr int kStaticBF = 3;
+constexpr int kStreamBF = 1;
 __device__ __forceinline__ double ld_sub_msg(const double *p) { return __builtin_nontemporal_load(p); }
 __device__ __forceinline__ void st_sub_msg(double *p, double v) { __builtin_nontemporal_store(v, p); }
 
@@ -220,7 +226,7 @@ __device__ __forceinline__ void sub_stage_commit(const SubCtx<Q> &c, int q, int 
 // some lane's own edge has |t| <= 1e-10 (:159).  E_old is requested first
 // (independent of the column indices), then the indices, then the posterior
 // gather that needs them.
-template <int Q>
+template <int Q, int BF>
 __device__ __forceinline__ bool sub_p1(const SubCtx<Q> &c, int r, const SubChunk &rc, double (&t)[SubCfg<Q>::K]) {
     constexpr int K = SubCfg<Q>::K;
     bool tiny = false;
@@ -231,7 +237,7 @@ __device__ __forceinline__ bool sub_p1(const SubCtx<Q> &c, int r, const SubChunk
         double eo[K];
 #pragma unroll
         for (int i = 0; i < K; ++i) {
-            {
+            if ((BF & 1) || i - i % kSG < rc.CS) {  // guarded form: every slot of a group that runs
                 eo[i] = (c.first || c.fresh) ? 0.0 : ld_sub_msg(sub_e(c, sub_edge(c, rc, i)));
                 col[i] = sub_lcol(c, r, rc, i);
             }
@@ -239,13 +245,13 @@ __device__ __forceinline__ bool sub_p1(const SubCtx<Q> &c, int r, const SubChunk
         const char *Lsrc = c.first ? c.Cu : c.Lu;  // iteration 0: M = ch (:85-90); uniform
 #pragma unroll
         for (int i = 0; i < K; ++i)
-            t[i] = ld_l2((const double *)(Lsrc + sub_off(c, col[i])));
+            if ((BF & 1) || i - i % kSG < rc.CS) t[i] = ld_l2((const double *)(Lsrc + sub_off(c, col[i])));
         // tanh in groups of kSG slots evaluated in lockstep (np_tanh_n: the
         // groups' table reads overlap); a group runs if its first slot is in
         // the chunk (slots past CS hold clamped, valid data and end as 1.0)
 #pragma unroll
         for (int g0 = 0; g0 < K; g0 += kSG) {
-            {
+            if ((BF & 1) || g0 < rc.CS) {
                 constexpr int G0 = kSG;
                 double d[G0];
 #pragma unroll
@@ -374,7 +380,7 @@ __device__ __forceinline__ void sub_hop(const SubCtx<Q> &c, int r, const double 
 
 // P3: E_new of this lane's slots of row r, stored and folded into S; the
 // identity column's posterior and z^1 bit.
-template <int Q>
+template <int Q, int BF>
 __device__ __forceinline__ void sub_p3_body(SubCtx<Q> &c, int r, double (&t)[SubCfg<Q>::K]) {
     constexpr int F = SubCfg<Q>::F, K = SubCfg<Q>::K;
     const SubChunk rc = sub_chunk(c.row_ptr, r, c.wave, Q);
@@ -396,7 +402,8 @@ __device__ __forceinline__ void sub_p3_body(SubCtx<Q> &c, int r, double (&t)[Sub
     const int nj = sub_nj(c, rc);
     int col[K];
 #pragma unroll
-    for (int i = 0; i < K; ++i) col[i] = sub_lcol(c, r, rc, i);  // clamped position: valid for every slot
+    for (int i = 0; i < K; ++i)
+        if ((BF & 2) || i < rc.CS) col[i] = sub_lcol(c, r, rc, i);  // clamped position: valid for every slot
     if (!tiny_row && div_nr_ok(P)) {  // the IEEE quotient without the scaling steps (cn_common.h)
 #pragma unroll
         for (int i = 0; i < K; ++i)
@@ -447,24 +454,40 @@ __device__ __forceinline__ void sub_p3_body(SubCtx<Q> &c, int r, double (&t)[Sub
     // lanes of a row share (col, frame)); the identity edge goes to `dummy`
     double EnI = 0.0;
     int colI = -1;
-    double *sp[K];
-    double sv[K];
+    if constexpr ((BF & 2) != 0) {
+        double *sp[K];
+        double sv[K];
 #pragma unroll
-    for (int i = 0; i < K; ++i) {
-        const bool own = i < nj;  // nj <= CS
-        const bool a = own && col[i] < c.k;
-        sp[i] = a ? c.S + (size_t)col[i] * F : c.dummy;
-        if (own && !a) {
-            EnI = t[i];
-            colI = col[i];
+        for (int i = 0; i < K; ++i) {
+            const bool own = i < nj;  // nj <= CS
+            const bool a = own && col[i] < c.k;
+            sp[i] = a ? c.S + (size_t)col[i] * F : c.dummy;
+            if (own && !a) {
+                EnI = t[i];
+                colI = col[i];
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < K; ++i) sv[i] = *sp[i];
+#pragma unroll
+        for (int i = 0; i < K; ++i) sv[i] = sv[i] + t[i];
+#pragma unroll
+        for (int i = 0; i < K; ++i) *sp[i] = sv[i];
+    } else {
+#pragma unroll
+        for (int i = 0; i < K; ++i) {
+            if (i < rc.CS) {
+                const bool own = i < nj;
+                const bool a = own && col[i] < c.k;
+                double *sp = a ? c.S + (size_t)col[i] * F : c.dummy;
+                *sp = *sp + t[i];
+                if (own && !a) {
+                    EnI = t[i];
+                    colI = col[i];
+                }
+            }
         }
     }
-#pragma unroll
-    for (int i = 0; i < K; ++i) sv[i] = *sp[i];
-#pragma unroll
-    for (int i = 0; i < K; ++i) sv[i] = sv[i] + t[i];
-#pragma unroll
-    for (int i = 0; i < K; ++i) *sp[i] = sv[i];
     if (colI >= 0) {  // identity column: L = ch + (0 + E) (:173-185)
         const double Lj = *sub_c(c, colI) + (0.0 + EnI);
         if (c.live) *sub_l(c, colI) = Lj;
@@ -477,22 +500,22 @@ __device__ __forceinline__ void sub_p3_body(SubCtx<Q> &c, int r, double (&t)[Sub
 
 // P3 of row r; in hop-first order its S additions wait until every
 // wavefront's P3 of row r-1 is complete (count per row g = pass*m + r)
-template <int Q>
+template <int Q, int BF>
 __device__ __forceinline__ void sub_p3(SubCtx<Q> &c, int r, double (&t)[SubCfg<Q>::K]) {
     const int g = c.ep0 + r;
     if (g > 0) wait_ge<false>(c.p3n + ((g - 1) & 3), kSW * (((g - 1) >> 2) + 1));
-    sub_p3_body(c, r, t);
+    sub_p3_body<Q, BF>(c, r, t);
     lds_release();  // this row's S additions before the count
     if ((threadIdx.x & 63) == 0)
         __hip_atomic_fetch_add(c.p3n + (g & 3), 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
-template <int Q>
+template <int Q, int BF>
 __device__ __forceinline__ void sub_body(SubCtx<Q> &c, int r, int m, double (&tcur)[SubCfg<Q>::K], bool ycur,
                                          double (&toth)[SubCfg<Q>::K], bool &yoth) {
     if (r < m) sub_hop(c, r, tcur, ycur);
-    if (r >= 1) sub_p3(c, r - 1, toth);
-    if (r + 1 < m) yoth = sub_p1(c, r + 1, sub_chunk(c.row_ptr, r + 1, c.wave, Q), toth);
+    if (r >= 1) sub_p3<Q, BF>(c, r - 1, toth);
+    if (r + 1 < m) yoth = sub_p1<Q, BF>(c, r + 1, sub_chunk(c.row_ptr, r + 1, c.wave, Q), toth);
 }
 
 template <int Q>
@@ -571,11 +594,11 @@ __global__ __launch_bounds__(64 * kSW, 1) void tile_sub_kernel(DevGraph g, DevSt
         bool yA = false, yB = false;
         if (m > 0) {
             sub_stage_commit(c, 0, sub_stage_issue(c, 0));
-            yA = sub_p1(c, 0, sub_chunk(row_ptr, 0, wave, Q), tA);
+            yA = sub_p1<Q, kStaticBF>(c, 0, sub_chunk(row_ptr, 0, wave, Q), tA);
         }
         for (int r = 0; r <= m; r += 2) {
-            sub_body(c, r, m, tA, yA, tB, yB);
-            if (r + 1 <= m) sub_body(c, r + 1, m, tB, yB, tA, yA);
+            sub_body<Q, kStaticBF>(c, r, m, tA, yA, tB, yB);
+            if (r + 1 <= m) sub_body<Q, kStaticBF>(c, r + 1, m, tB, yB, tA, yA);
         }
         __syncthreads();  // every P3 done: S complete, identity bits set
 
@@ -763,11 +786,11 @@ __global__ __launch_bounds__(64 * kSW, 1) void tile_sub_stream_kernel(
         bool yA = false, yB = false;
         if (m > 0) {
             sub_stage_commit(c, 0, sub_stage_issue(c, 0));
-            yA = sub_p1(c, 0, sub_chunk(row_ptr, 0, wave, Q), tA);
+            yA = sub_p1<Q, kStreamBF>(c, 0, sub_chunk(row_ptr, 0, wave, Q), tA);
         }
         for (int r = 0; r <= m; r += 2) {
-            sub_body(c, r, m, tA, yA, tB, yB);
-            if (r + 1 <= m) sub_body(c, r + 1, m, tB, yB, tA, yA);
+            sub_body<Q, kStreamBF>(c, r, m, tA, yA, tB, yB);
+            if (r + 1 <= m) sub_body<Q, kStreamBF>(c, r + 1, m, tB, yB, tA, yA);
         }
         __syncthreads();
 
