@@ -152,11 +152,8 @@ __device__ __forceinline__ double tile_load_e(const TileCtx &c, const RowChunk &
 }
 __device__ __forceinline__ bool tile_t(const TileCtx &c, double &t, double eo) {
     const double M = c.first ? t : t - (c.fresh ? 0.0 : eo);  // :85-90 / :260-268
-    // tanh evaluated for every lane, the +-17.5 clip as selects (straight-line
-    // code across the chunk's edges)
-    const double d = M * 0.5;
-    const double r = np_tanh(d, c.ttab);
-    t = d > 17.5 ? kCL : (d < -17.5 ? -kCL : r);  // :138-146 (cn_tanh, as selects)
+    // tanh evaluated for every lane, the +-17.5 clip on the output (cn_tanh)
+    t = tanh_clip(np_tanh(M * 0.5, c.ttab));  // :138-146
     return !(fabs(t) > kTiny);
 }
 

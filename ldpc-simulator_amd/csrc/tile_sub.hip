@@ -268,7 +268,7 @@ __device__ __forceinline__ bool sub_p1(const SubCtx<Q> &c, int r, const SubChunk
                 for (int q = 0; q < G0; ++q) {
                     const int i = g0 + q;
                     if (i < K) {
-                        const double tv = d[q] > 17.5 ? kCL : (d[q] < -17.5 ? -kCL : th[q]);  // :138-146
+                        const double tv = tanh_clip(th[q]);  // :138-146 (cn_common.h)
                         tiny |= i < nj && !(fabs(tv) > kTiny);
                         // slots past this lane's piece: 1.0, an exact no-op in the chain product
                         t[i] = i < nj ? tv : 1.0;

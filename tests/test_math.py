@@ -55,6 +55,23 @@ def test_device_tanh_equals_numpy_tanh(host_math):
     assert np.signbit(_run(host_math.host_np_tanh, np.array([-0.0]))[0])
 
 
+def test_tanh_output_clip_equals_input_clip(host_math):
+    """cn_common.h tanh_clip: clip(np_tanh(d), -CL, CL) is the reference's
+    input clip (spa_decoder.py:138-146: d > 17.5 -> CL, d < -17.5 -> -CL)
+    bit for bit -- np.tanh(17.5) == CL and np_tanh is monotone across +-17.5."""
+    assert np.tanh(17.5) == CL and _run(host_math.host_np_tanh, np.array([17.5]))[0] == CL
+    base = np.float64(17.5).view(np.int64)
+    k = np.arange(2_000_000, dtype=np.int64)
+    rng = np.random.default_rng(11)
+    x = np.concatenate([(base + k).view(np.float64), (base - k).view(np.float64)])
+    x = np.concatenate([x, -x, rng.uniform(-40, 40, 1_000_000),
+                        10 ** rng.uniform(0, 308, 200_000) * rng.choice([-1, 1], 200_000),
+                        [np.inf, -np.inf, 1.7e308, -1.7e308, 24.0, -24.0]])
+    y = _run(host_math.host_np_tanh, x)
+    sel = np.where(x > 17.5, CL, np.where(x < -17.5, -CL, y))
+    np.testing.assert_array_equal(np.clip(y, -CL, CL).view(np.int64), sel.view(np.int64))
+
+
 def test_oracle_tanh_equals_numpy_tanh():
     import oracle
     x = _tanh_inputs(400_000, seed=9)
