@@ -7,6 +7,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <climits>
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
@@ -93,6 +94,54 @@ struct DeviceGuard {
         if (prev >= 0) (void)hipSetDevice(prev);
     }
 };
+
+// Sub-tile decoder's S order (tile_sub.hip sub_p3): wavefront w's P3 of row r
+// waits for row r-1's P3 by wavefronts [lo, hi], those whose chunk's extended
+// column span (from just past the previous non-empty chunk's last column to
+// its own last column; the last non-empty chunk runs to infinity) overlaps
+// w's.  Chunking as sub_chunk: C = ceil(deg / 16) edges per wavefront.  An
+// empty chunk waits for nothing (lo > hi); after an empty row, every
+// wavefront waits for all 16 (whose in-order P3s then cover every row before).
+std::vector<int> sub_p3_deps(int m, const int *row_ptr, const int *col_idx) {
+    constexpr int W = ldpc::kSubWaves;
+    std::vector<int> dep((size_t)m * W, 1);  // lo 1 > hi 0: no wait
+    auto spans = [&](int r, long long lo[W], long long hi[W], bool ne[W]) {
+        const int beg = row_ptr[r], deg = row_ptr[r + 1] - beg, C = (deg + W - 1) / W;
+        long long prev = -1;
+        int last = -1;
+        for (int w = 0; w < W; ++w) {
+            const int cnt = std::max(0, std::min(deg - w * C, C));
+            ne[w] = cnt > 0;
+            if (!ne[w]) continue;
+            lo[w] = prev + 1;
+            hi[w] = prev = col_idx[beg + w * C + cnt - 1];
+            last = w;
+        }
+        if (last >= 0) hi[last] = LLONG_MAX;
+        return last >= 0;
+    };
+    long long plo[W], phi[W], lo[W], hi[W];
+    bool pne[W], ne[W];
+    bool prev_any = m > 0 && spans(0, plo, phi, pne);
+    for (int r = 1; r < m; ++r) {
+        spans(r, lo, hi, ne);
+        for (int w = 0; w < W; ++w) {
+            if (!ne[w]) continue;
+            int vlo = W, vhi = -1;
+            for (int v = 0; v < W; ++v)
+                if (!prev_any || (pne[v] && plo[v] <= hi[w] && lo[w] <= phi[v])) {
+                    vlo = std::min(vlo, v);
+                    vhi = std::max(vhi, v);
+                }
+            dep[(size_t)r * W + w] = vlo > vhi ? 1 : (vlo | vhi << 8);
+        }
+        std::copy(lo, lo + W, plo);
+        std::copy(hi, hi + W, phi);
+        std::copy(ne, ne + W, pne);
+        prev_any = std::any_of(ne, ne + W, [](bool b) { return b; });
+    }
+    return dep;
+}
 
 int require_gpu() {
     int n = 0;
@@ -343,7 +392,8 @@ int ldpc_graph_create(int32_t m, int32_t n, const int32_t *row_ptr, const int32_
     g->device = device;
     DeviceGuard dg(device);
     if (device < 0) (void)hipGetDevice(&g->device);
-    const size_t nints = (size_t)(m + 1) + nnz + (size_t)(n + 1) + 2 * (size_t)nnz;
+    const std::vector<int> p3dep = sub_p3_deps(m, row_ptr, col_idx);
+    const size_t nints = (size_t)(m + 1) + nnz + (size_t)(n + 1) + 2 * (size_t)nnz + p3dep.size();
     if (int rc = dev_alloc(&g->d_ints, nints)) {
         delete g;
         return rc;
@@ -367,12 +417,16 @@ int ldpc_graph_create(int32_t m, int32_t n, const int32_t *row_ptr, const int32_
     G.csc_edge = p;
     p += nnz;
     G.csc_row = p;
+    p += nnz;
+    G.p3dep = p;
     hipError_t e = hipSuccess;
     if (e == hipSuccess) e = hipMemcpy((void *)G.row_ptr, row_ptr, sizeof(int) * (m + 1), hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMemcpy((void *)G.col_idx, col_idx, sizeof(int) * nnz, hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMemcpy((void *)G.csc_ptr, csc_ptr.data(), sizeof(int) * (n + 1), hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMemcpy((void *)G.csc_edge, csc_edge.data(), sizeof(int) * nnz, hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMemcpy((void *)G.csc_row, csc_row.data(), sizeof(int) * nnz, hipMemcpyHostToDevice);
+    if (e == hipSuccess && m > 0)
+        e = hipMemcpy((void *)G.p3dep, p3dep.data(), sizeof(int) * p3dep.size(), hipMemcpyHostToDevice);
     if (e == hipSuccess && std_form && k > 0) {  // encoder table: A bit-packed per row
         const size_t kw = (size_t)(k + 31) / 32;
         std::vector<uint32_t> ap((size_t)m * kw, 0u);

@@ -21,6 +21,10 @@ namespace ldpc {
 
 constexpr int kTile = 64;  // frames per tile == wavefront width on CDNA
 
+// wavefronts per sub-tile workgroup (tile_sub.hip); the host builds the
+// P3 order table (DevGraph::p3dep) for this chunking
+constexpr int kSubWaves = 16;
+
 struct DevGraph {
     int m, n, k, nnz;
     int max_row_deg, max_col_deg;
@@ -32,6 +36,7 @@ struct DevGraph {
     const int *csc_edge;     // [nnz] CSR edge id, rows ascending within a column
     const int *csc_row;      // [nnz] row of that edge
     const uint32_t *a_packed;  // [m][kw] bit j of row r = A[r][j] (encoder; std_form only)
+    const int *p3dep;          // [m][16] sub-tile S order: lo | hi << 8 (tile_sub.hip sub_p3)
 };
 
 struct DevState {

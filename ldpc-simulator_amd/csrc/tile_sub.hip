@@ -49,7 +49,7 @@
 namespace ldpc {
 namespace {
 
-constexpr int kSW = 16;                 // wavefronts per workgroup
+constexpr int kSW = kSubWaves;          // wavefronts per workgroup (spa_device.h)
 constexpr size_t kSubLdsMax = 163840;
 
 template <int Q>
@@ -111,8 +111,8 @@ __host__ __device__ inline SubLayout sub_layout(int k, int m, int F) {
     o = al16(o + (size_t)((m + 31) / 32) * F * sizeof(uint32_t));
     t.lane_i = o;  // bad[F], nllr count[F], live[F]
     o = al16(o + 3 * (size_t)F * sizeof(int));
-    t.flags = o;  // chain flag[kSR], tiny[kSR], tiny sequence, running, P3 counts[4]
-    o = al16(o + (2 * kSR + 6) * sizeof(int));
+    t.flags = o;  // chain flag[kSR], tiny[kSR], tiny sequence, running, P3 rows done[kSW]
+    o = al16(o + (2 * kSR + 2 + kSW) * sizeof(int));
     t.dummy = o;  // [F] target of the identity lane's masked-off S update
     o = al16(o + (size_t)F * sizeof(double));
     t.cidx = o;  // [kCRing][kSW][64/F * K] uint16 column indices (one wavefront chunk per row)
@@ -152,7 +152,8 @@ struct SubCtx {
     uint32_t *ib;   // LDS, word w at [w * F]
     uint16_t *cidx; // LDS, this wavefront's index ring: row slot s, position p at [s * kSW * Q * K + p]
     int m;
-    int *flag, *tinyf, *tseq, *p3n;
+    int *flag, *tinyf, *tseq, *p3row;
+    const int *p3dep;
     LdsTanh ttab;
     LdsLog ltab;
     AtanhCoef ac;
@@ -498,16 +499,26 @@ __device__ __forceinline__ void sub_p3_body(SubCtx<Q> &c, int r, double (&t)[Sub
     }
 }
 
-// P3 of row r; in hop-first order its S additions wait until every
-// wavefront's P3 of row r-1 is complete (count per row g = pass*m + r)
+// P3 of row r.  S_col must take its additions rows ascending.  Wavefront w's
+// chunk of row r spans columns [first, last]; extended to the gap before it,
+// the chunks of a row partition the columns, so waiting for row r-1's P3 by
+// exactly the wavefronts whose extended spans overlap w's (g.p3dep, built on
+// the host: ldpc_api.cpp sub_p3_deps) orders every column's additions by
+// induction over the rows -- the neighbours, not all 16 wavefronts (the full
+// row barrier this replaces cost early wavefronts up to 39 % of their time,
+// profiles/r2an_phase_timers).  p3row[v] = 1 + the last global row (pass*m + r)
+// whose P3 wavefront v finished; passes are separated by __syncthreads.
 template <int Q, int BF>
 __device__ __forceinline__ void sub_p3(SubCtx<Q> &c, int r, double (&t)[SubCfg<Q>::K]) {
     const int g = c.ep0 + r;
-    if (g > 0) wait_ge<false>(c.p3n + ((g - 1) & 3), kSW * (((g - 1) >> 2) + 1));
+    if (r > 0) {  // row r-1's P3 by the wavefronts whose column spans overlap ours
+        const int d = c.p3dep[r * kSW + c.wave];
+        for (int v = d & 0xff; v <= (d >> 8); ++v) wait_ge<false>(c.p3row + v, g);
+    }
     sub_p3_body<Q, BF>(c, r, t);
     lds_release();  // this row's S additions before the count
     if ((threadIdx.x & 63) == 0)
-        __hip_atomic_fetch_add(c.p3n + (g & 3), 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        lds_st(c.p3row + c.wave, g + 1);
 }
 
 template <int Q, int BF>
@@ -542,7 +553,7 @@ __global__ __launch_bounds__(64 * kSW, 1) void tile_sub_kernel(DevGraph g, DevSt
     for (int i = threadIdx.x; i < (kw + mw) * F; i += blockDim.x) zb[i] = 0u;
     for (int i = threadIdx.x; i < 2 * F; i += blockDim.x) bad[i] = 0;
     if (threadIdx.x < 2 * kSR) flags[threadIdx.x] = -1;
-    if (threadIdx.x >= 2 * kSR && threadIdx.x < 2 * kSR + 6) flags[threadIdx.x] = 0;
+    if (threadIdx.x >= 2 * kSR && threadIdx.x < 2 * kSR + 2 + kSW) flags[threadIdx.x] = 0;
     const int lane = threadIdx.x & 63;
     const int wave = uniform(threadIdx.x >> 6);
     const int j = lane / F, f = lane % F;
@@ -572,7 +583,8 @@ __global__ __launch_bounds__(64 * kSW, 1) void tile_sub_kernel(DevGraph g, DevSt
     c.flag = flags;
     c.tinyf = flags + kSR;
     c.tseq = flags + 2 * kSR;
-    c.p3n = flags + 2 * kSR + 2;
+    c.p3row = flags + 2 * kSR + 2;
+    c.p3dep = g.p3dep;
     c.ttab = LdsTanh{mlds.tanh};
     c.ltab = LdsLog{mlds.log};
     c.ac = ac;
@@ -705,7 +717,7 @@ __global__ __launch_bounds__(64 * kSW, 1) void tile_sub_stream_kernel(
     for (int i = threadIdx.x; i < (kw + mw) * F; i += blockDim.x) zb[i] = 0u;
     for (int i = threadIdx.x; i < 2 * F; i += blockDim.x) bad[i] = 0;
     if (threadIdx.x < 2 * kSR) flags[threadIdx.x] = -1;
-    if (threadIdx.x >= 2 * kSR && threadIdx.x < 2 * kSR + 6) flags[threadIdx.x] = 0;
+    if (threadIdx.x >= 2 * kSR && threadIdx.x < 2 * kSR + 2 + kSW) flags[threadIdx.x] = 0;
     const int lane = threadIdx.x & 63;
     const int wave = uniform(threadIdx.x >> 6);
     const int j = lane / F, f = lane % F;
@@ -739,7 +751,8 @@ __global__ __launch_bounds__(64 * kSW, 1) void tile_sub_stream_kernel(
     c.flag = flags;
     c.tinyf = flags + kSR;
     c.tseq = flags + 2 * kSR;
-    c.p3n = flags + 2 * kSR + 2;
+    c.p3row = flags + 2 * kSR + 2;
+    c.p3dep = g.p3dep;
     c.ttab = LdsTanh{mlds.tanh};
     c.ltab = LdsLog{mlds.log};
     c.ac = ac;
