@@ -168,7 +168,10 @@ int ensure_messages(ldpc_decoder *d) {
     if (d->E) return LDPC_OK;
     const DevGraph &G = d->g->dg;
     const size_t cap = (size_t)d->cap_tiles * kTile;
-    int rc = dev_alloc(&d->E, cap * (size_t)G.nnz);
+    // + kEPadEdges edges of slack: the sub-tile decoder's P1 loads every
+    // register slot of a lane group unclamped (tile_sub.hip, sub_p1), up to 63
+    // edges past a row's end -- past the last tile's region on its last row
+    int rc = dev_alloc(&d->E, cap * (size_t)G.nnz + (size_t)ldpc::kEPadEdges * kTile);
     if (!rc) rc = dev_alloc(&d->T, (size_t)d->nslots * G.max_row_deg * kTile);
     if (rc) {
         (void)hipFree(d->E);

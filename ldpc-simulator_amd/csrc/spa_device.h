@@ -24,6 +24,9 @@ constexpr int kTile = 64;  // frames per tile == wavefront width on CDNA
 // wavefronts per sub-tile workgroup (tile_sub.hip); the host builds the
 // P3 order table (DevGraph::p3dep) for this chunking
 constexpr int kSubWaves = 16;
+// message-array slack (edges x 64 lanes) past the last tile: the sub-tile
+// decoder's unclamped slot loads overshoot a row by < Q*K = 64 edges
+constexpr int kEPadEdges = 128;
 
 struct DevGraph {
     int m, n, k, nnz;

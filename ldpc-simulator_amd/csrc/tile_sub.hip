@@ -184,10 +184,6 @@ __device__ __forceinline__ uint32_t sub_off(const SubCtx<Q> &c, int item) {
     return ((uint32_t)item << 9) + c.lo8;
 }
 template <int Q>
-__device__ __forceinline__ double *sub_e(const SubCtx<Q> &c, int edge) {
-    return (double *)(c.Eu + sub_off(c, edge));
-}
-template <int Q>
 __device__ __forceinline__ double *sub_l(const SubCtx<Q> &c, int col) {
     return (double *)(c.Lu + sub_off(c, col));
 }
@@ -199,10 +195,26 @@ template <int Q>
 __device__ __forceinline__ int sub_col(const SubCtx<Q> &c, int edge) {
     return *(const int *)((const char *)c.col_idx + ((uint32_t)edge << 2));
 }
-// column of this lane's slot i of row r (chunk rc), from the staged ring
+// This lane's piece of row r's staged column indices: slot i at [i].  The
+// staging wrote every position < Q*K (past the chunk: the clamped last
+// column), and j*CS + i < Q*K for every slot, so no clamp is needed here and
+// each slot's read is an immediate offset from one address per row.
 template <int Q>
-__device__ __forceinline__ int sub_lcol(const SubCtx<Q> &c, int r, const SubChunk &rc, int i) {
-    return c.cidx[(r % kCRing) * kSW * Q * SubCfg<Q>::K + min(c.j * rc.CS + i, rc.cnt - 1)];
+__device__ __forceinline__ const uint16_t *sub_lcols(const SubCtx<Q> &c, int r, const SubChunk &rc) {
+    return c.cidx + (r % kCRing) * kSW * Q * SubCfg<Q>::K + c.j * rc.CS;
+}
+// Byte offset of this lane's slot 0 of chunk rc in the tile's E; slot i is at
+// + i * 512 (an immediate offset).  Slots past the lane's piece are NOT
+// clamped: their loads read other edges (or, on the last tile's last row, the
+// allocation's kEPadEdges slack) and their values are discarded (t = 1.0, no
+// store).
+template <int Q>
+__device__ __forceinline__ uint32_t sub_eoff(const SubCtx<Q> &c, const SubChunk &rc) {
+    return ((uint32_t)(rc.c0 + c.j * rc.CS) << 9) + c.lo8;
+}
+template <int Q>
+__device__ __forceinline__ double *sub_es(const SubCtx<Q> &c, uint32_t off, int i) {
+    return (double *)(c.Eu + (size_t)off + (size_t)i * (kTile * sizeof(double)));
 }
 // Staging of row q's indices into the ring: issue (one index per lane, lanes <
 // the chunk size) early, commit to LDS once the wavefront has waited on its
@@ -234,13 +246,18 @@ __device__ __forceinline__ bool sub_p1(const SubCtx<Q> &c, int r, const SubChunk
     const int sv = sub_stage_issue(c, r + 1);  // row r+1's indices, committed below
     if (rc.cnt > 0) {
         const int nj = sub_nj(c, rc);
+        const uint16_t *lc = sub_lcols(c, r, rc);
+        const uint32_t eoff = sub_eoff(c, rc);
+        // iteration 0 / a fresh streaming frame: M = L (E_old is loaded anyway
+        // and unused: L - 0.0 == L for every L)
+        const bool noE = c.first || c.fresh;
         int col[K];
         double eo[K];
 #pragma unroll
         for (int i = 0; i < K; ++i) {
             if ((BF & 1) || i - i % kSG < rc.CS) {  // guarded form: every slot of a group that runs
-                eo[i] = (c.first || c.fresh) ? 0.0 : ld_sub_msg(sub_e(c, sub_edge(c, rc, i)));
-                col[i] = sub_lcol(c, r, rc, i);
+                eo[i] = ld_sub_msg(sub_es(c, eoff, i));
+                col[i] = lc[i];
             }
         }
         const char *Lsrc = c.first ? c.Cu : c.Lu;  // iteration 0: M = ch (:85-90); uniform
@@ -258,7 +275,7 @@ __device__ __forceinline__ bool sub_p1(const SubCtx<Q> &c, int r, const SubChunk
 #pragma unroll
                 for (int q = 0; q < G0; ++q) {
                     const int i = g0 + q < K ? g0 + q : K - 1;
-                    const double M = c.first ? t[i] : t[i] - eo[i];  // :85-90 / :260-268
+                    const double M = noE ? t[i] : t[i] - eo[i];  // :85-90 / :260-268
                     d[q] = M * 0.5;
                 }
                 double th[G0];
@@ -401,10 +418,11 @@ __device__ __forceinline__ void sub_p3_body(SubCtx<Q> &c, int r, double (&t)[Sub
     }
     const double P = c.slot[s * F];
     const int nj = sub_nj(c, rc);
+    const uint16_t *lc = sub_lcols(c, r, rc);
     int col[K];
 #pragma unroll
     for (int i = 0; i < K; ++i)
-        if ((BF & 2) || i < rc.CS) col[i] = sub_lcol(c, r, rc, i);  // clamped position: valid for every slot
+        if ((BF & 2) || i < rc.CS) col[i] = lc[i];  // clamped copy past the chunk: a valid column
     if (!tiny_row && div_nr_ok(P)) {  // the IEEE quotient without the scaling steps (cn_common.h)
 #pragma unroll
         for (int i = 0; i < K; ++i)
@@ -447,9 +465,10 @@ __device__ __forceinline__ void sub_p3_body(SubCtx<Q> &c, int r, double (&t)[Sub
         }
     }
     if (c.live) {
+        const uint32_t eoff = sub_eoff(c, rc);
 #pragma unroll
         for (int i = 0; i < K; ++i)
-            if (i < rc.CS && i < nj) st_sub_msg(sub_e(c, sub_edge(c, rc, i)), t[i]);
+            if (i < rc.CS && i < nj) st_sub_msg(sub_es(c, eoff, i), t[i]);
     }
     // S_col += E_new, rows ascending (a column occurs once per row: no two
     // lanes of a row share (col, frame)); the identity edge goes to `dummy`

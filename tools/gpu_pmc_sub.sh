@@ -3,6 +3,6 @@ export TMPDIR=/tmp
 O=gpurun_out/${TAG:-pmc}; mkdir -p $O
 timeout -s KILL 60 rocprofv3 -L > $O/counters.txt 2>&1 || true
 B="--steps 1 --warmup 0 --frames 16384 --cpu-seconds 0 --extra-snr= --iters 10"
-timeout -s KILL 120 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_SALU --output-format csv -d $O/p1 -o run -- python3 bench.py $B > $O/p1.log 2>&1 || exit 1
+timeout -s KILL 120 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_SALU GRBM_GUI_ACTIVE --output-format csv -d $O/p1 -o run -- python3 bench.py $B > $O/p1.log 2>&1 || exit 1
 timeout -s KILL 120 rocprofv3 --pmc SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_SMEM SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_ACTIVE_INST_LDS --output-format csv -d $O/p2 -o run -- python3 bench.py $B > $O/p2.log 2>&1 || exit 1
 echo done
