@@ -15,20 +15,22 @@
 // 0..CS-1.  The left-to-right product P = t0 * t1 * ... (:151-152) crosses lane
 // groups inside the wavefront: starting from the prefix P of the wavefront
 // before it, every lane multiplies its own slots in order; lane group j's
-// result is the prefix through group j, broadcast to all lanes (ds_bpermute)
-// before group j+1's turn.  Groups with no edges are skipped.  The rest is
-// tile_kernel's pipeline and ordering argument unchanged:
+// result is the prefix through group j, moved to group j+1 (permlane swaps;
+// ds_bpermute for Q = 8)
+// before group j+1's turn.  Groups with no edges are skipped.  Each wavefront
+// runs the hop-first pipeline
 //
-//   body(r):  P3(r-1)  E_new = 2 atanh(clip(P/t)) (:159-168), stored, added
-//                      into S (LDS, per lane: column of its edge, its frame);
-//             hop(r)   this wavefront's piece of row r's product;
+//   body(r):  hop(r)   this wavefront's piece of row r's product;
+//             P3(r-1)  E_new = 2 atanh(clip(P/t)) (:159-168), stored, added
+//                      into S (LDS, per lane: column of its edge, its frame)
+//                      after the overlapping wavefronts' P3(r-2) (sub_p3);
 //             P1(r+1)  L[col], E_old, t = tanh((L - E_old)/2) (:138-146,
 //                      :260-268).
 //
-// Opt-in (LDPC_TILE_SUB=1): bit-identical to the split path, but slower on
-// every 2304 code measured -- the in-wavefront hand-over costs
-// Q rounds of products and two ds_bpermute per hop on the row's critical path,
-// and F = 8 reads half cache lines.
+// The default decoder of wimax_2304_0.5 (F = 16, Q = 4: the product crosses
+// lane groups with v_permlane16/32_swap); bit-identical to the split path.
+// The F = 8 form (Q = 8, ds_bpermute hand-over) for the r3/4 codes is opt-in
+// (LDPC_TILE_SUB=1): slower than the split path there.
 //
 // Per edge and iteration the HBM traffic is the algorithmic 16 B (E_old read,
 // E_new write) plus the L[col] gather (8 B, L2/MALL): the split CN/VN
