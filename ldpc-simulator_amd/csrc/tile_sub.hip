@@ -86,6 +86,13 @@ constexpr int kSG = 1;
 // (+3.4 % at 2 dB) but loses 8 % to bit 1 (profiles/r2ag_stream_bf).
 constexpr int kStaticBF = 3;
 constexpr int kStreamBF = 1;
+// Logical wavefront (chunk position in a row) of hardware wavefront hw: the
+// four wavefronts of one SIMD (hw = s, s+4, s+8, s+12) take four consecutive
+// chunk positions, so each SIMD holds one contiguous quarter of every row's
+// chain and its P3 neighbours.  +1.3 % over the identity map, static and
+// streaming (profiles/r2at_wave_map; pairs of positions per SIMD measured the
+// same, spin waits at a lower issue priority +0.2 %).
+__device__ __forceinline__ int sub_wave(int hw) { return (hw & 3) * 4 + (hw >> 2); }
 __device__ __forceinline__ double ld_sub_msg(const double *p) { return __builtin_nontemporal_load(p); }
 __device__ __forceinline__ void st_sub_msg(double *p, double v) { __builtin_nontemporal_store(v, p); }
 
@@ -576,7 +583,7 @@ __global__ __launch_bounds__(64 * kSW, 1) void tile_sub_kernel(DevGraph g, DevSt
     if (threadIdx.x < 2 * kSR) flags[threadIdx.x] = -1;
     if (threadIdx.x >= 2 * kSR && threadIdx.x < 2 * kSR + 2 + kSW) flags[threadIdx.x] = 0;
     const int lane = threadIdx.x & 63;
-    const int wave = uniform(threadIdx.x >> 6);
+    const int wave = uniform(sub_wave(threadIdx.x >> 6));
     const int j = lane / F, f = lane % F;
     const int fr = tile * kTile + sub * F + f;  // this lane's frame
     if (wave == 0 && j == 0) livel[f] = st.done[fr] == 0 ? 1 : 0;
@@ -740,7 +747,7 @@ __global__ __launch_bounds__(64 * kSW, 1) void tile_sub_stream_kernel(
     if (threadIdx.x < 2 * kSR) flags[threadIdx.x] = -1;
     if (threadIdx.x >= 2 * kSR && threadIdx.x < 2 * kSR + 2 + kSW) flags[threadIdx.x] = 0;
     const int lane = threadIdx.x & 63;
-    const int wave = uniform(threadIdx.x >> 6);
+    const int wave = uniform(sub_wave(threadIdx.x >> 6));
     const int j = lane / F, f = lane % F;
     const int lane64 = sub * F + f;
     const bool slot_lane = wave == 0 && j == 0;  // the lane that owns frame slot f
