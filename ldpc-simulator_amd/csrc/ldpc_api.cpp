@@ -71,6 +71,8 @@ struct ldpc_decoder {
     unsigned long long *counters = nullptr;  // [counters_cap] + 1 frame-index counter (streaming)
     int counters_cap = 0;
     int *cpairs = nullptr;  // streaming tail compaction plan (1 + 2 cap ints), on first use
+    uint32_t *tzb = nullptr;  // streaming tail VN: z^1 bits [cap_tiles][ceil(n/32)][64], zero between uses
+    int *tcnt = nullptr;      // streaming tail VN: normalized-LLR counts [cap_tiles*64], zero between uses
     DevState st{};
     // profiling (ldpc_profile_*)
     bool prof = false;
@@ -542,6 +544,8 @@ int ldpc_decoder_destroy(ldpc_decoder *d) {
     (void)hipFree(d->T);
     (void)hipFree(d->rare);
     (void)hipFree(d->cpairs);
+    (void)hipFree(d->tzb);
+    (void)hipFree(d->tcnt);
     (void)hipFree(d->L);
     (void)hipFree(d->ch);
     (void)hipFree(d->ints);
@@ -742,6 +746,30 @@ int ldpc_generate_frames(ldpc_decoder *d, uint64_t seed, int32_t snr_point, doub
 
 namespace {
 
+// Streaming tail: the column-parallel VN (launch_vn_tail) replaces vn_kernel
+// once at most kTailTiles tiles run; the sub-tile streaming kernel hands its
+// frames over once the supply is out and at most LDPC_HANDOFF frames still
+// run (default: handoff_frames).  LDPC_TAIL_VN=0 / LDPC_HANDOFF=0 switch them off.
+constexpr int kTailTiles = 128;
+bool tail_vn_enabled() {
+    const char *e = getenv("LDPC_TAIL_VN");
+    return !e || atoi(e) != 0;
+}
+// Default: once the supply is out and at most 3/5 of the slots the sub-tile
+// kernel keeps resident (one 16-frame workgroup per CU) still run.  At 3 dB
+// (wimax_2304_0.5) that is within a few passes -- about 2/3 of the slots then
+// hold frames that will fail, at every stage of their 50 passes -- and the
+// step takes 615 ms instead of 1.1 s; at 2 dB, where nearly every slot runs to
+// 50 passes, the sub-tile kernel keeps the bulk (3/4: -2 % there;
+// profiles/r2au_tail).
+int64_t handoff_frames(int64_t slots) {
+    const char *e = getenv("LDPC_HANDOFF");
+    if (e) return atoll(e);
+    int dev = 0, cus = 256;
+    if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    return std::min<int64_t>(slots, (int64_t)cus * 16) * 3 / 5;
+}
+
 // Streaming schedule of one SNR point: the decoder's cap frames are slots.  A
 // slot whose frame finishes (vn_kernel) is refilled with the next frame index
 // (refill_kernel), so no slot waits for the slowest frame of its tile or
@@ -756,21 +784,51 @@ int mc_stream_point(ldpc_decoder *d, uint64_t seed, int p, double sigma, int64_t
     DevState st = d->st;
     unsigned long long *ctr = d->counters + (size_t)p * LDPC_MC_NCOUNT;
     unsigned long long *next = d->counters + d->counters_cap;
-    if (!split && ldpc::use_tile_stream(G) && st.ntiles <= st.nslots) {
-        // one launch: every workgroup's lanes pull frames until the supply is out
-        HIP_TRY(hipMemsetAsync(next, 0, sizeof(unsigned long long), s));
-        HIP_TRY(timed(d, LDPC_K_TILE, s, [&] {
-            return ldpc::launch_tile_stream(G, st, max_iter, nllr, seed, p, sigma, frame0, total, next, ctr, s);
-        }));
-        return LDPC_OK;
+    const int cap = d->cap_tiles * kTile;
+    // streaming tail VN (column-parallel, launch_vn_tail) once few tiles run
+    const bool tail_ok = G.a_packed && ((G.k + 31) >> 5) <= 64 && tail_vn_enabled();
+    if (tail_ok && !d->tzb) {
+        const size_t nzb = (size_t)d->cap_tiles * ((G.n + 31) / 32) * kTile;
+        if (dev_alloc(&d->tzb, nzb) || dev_alloc(&d->tcnt, (size_t)cap)) return LDPC_ENOMEM;
+        HIP_TRY(hipMemsetAsync(d->tzb, 0, nzb * sizeof(uint32_t), s));
+        HIP_TRY(hipMemsetAsync(d->tcnt, 0, (size_t)cap * sizeof(int), s));
     }
-    HIP_TRY(ldpc::launch_stream_init(G, st, s));
-    HIP_TRY(hipMemsetAsync(next, 0, sizeof(unsigned long long), s));
     auto refill = [&] {
         return timed(d, LDPC_K_GEN, s,
                      [&] { return ldpc::launch_refill(G, st, seed, p, sigma, frame0, total, next, s); });
     };
-    HIP_TRY(refill());
+    int cur = ntiles;  // tiles the steps launch (shrinks as the tail is compacted)
+    if (!split && ldpc::use_tile_stream(G) && st.ntiles <= st.nslots) {
+        // one launch: every workgroup's lanes pull frames until the supply is
+        // out; the sub-tile decoder hands its last running frames to the
+        // column-parallel tail below (one pass of a sub-tile costs ~14 ms)
+        const int64_t ho = tail_ok && ldpc::sub_frames(G) == 16 ? handoff_frames((int64_t)ntiles * kTile) : 0;
+        HIP_TRY(hipMemsetAsync(next, 0, sizeof(unsigned long long), s));
+        HIP_TRY(timed(d, LDPC_K_TILE, s, [&] {
+            return ldpc::launch_tile_stream(G, st, max_iter, nllr, seed, p, sigma, frame0, total, next, ctr, ho, s);
+        }));
+        if (ho <= 0) return LDPC_OK;
+        unsigned long long finished = 0;
+        HIP_TRY(hipMemcpyAsync(&finished, ctr, sizeof(finished), hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipStreamSynchronize(s));
+        if ((int64_t)finished >= total) return LDPC_OK;
+        // the running frames (split-path slot state, written by the kernel)
+        // move into the first tiles; the loop below continues them
+        const int nt = (int)((total - (int64_t)finished + kTile - 1) / kTile);
+        if (!d->cpairs && dev_alloc(&d->cpairs, 1 + 2 * (size_t)cap)) return LDPC_ENOMEM;
+        if (nt < cur) {
+            HIP_TRY(ldpc::launch_compact(G, st, nt, cap, d->cpairs, s));
+            state_bind(d, nt, nt * kTile);
+            st = d->st;
+            cur = nt;
+        } else {
+            HIP_TRY(ldpc::launch_compact(G, st, cur, cap, d->cpairs, s));  // tile_active of every tile
+        }
+    } else {
+        HIP_TRY(ldpc::launch_stream_init(G, st, s));
+        HIP_TRY(hipMemsetAsync(next, 0, sizeof(unsigned long long), s));
+        HIP_TRY(refill());
+    }
     HIP_TRY(hipMemsetAsync(st.rare_count, 0, sizeof(int) * 2, s));  // see run_iterations
     const int64_t slots = (int64_t)ntiles * kTile;
     const int64_t min_steps = (total + slots - 1) / slots;            // every slot needs >= 1 step per frame
@@ -781,7 +839,6 @@ int mc_stream_point(ldpc_decoder *d, uint64_t seed, int p, double sigma, int64_t
         const char *e = getenv("LDPC_COMPACT");
         return !e || atoi(e) != 0;
     }();
-    int cur = ntiles;  // tiles the steps launch (shrinks as the tail is compacted)
     for (;;) {
         // every frame fits in the slots: all start now and stop by max_iter
         const int64_t until = total <= slots ? std::max<int64_t>(step + kPoll, max_iter)
@@ -790,7 +847,11 @@ int mc_stream_point(ldpc_decoder *d, uint64_t seed, int p, double sigma, int64_t
             const int par = (int)(step & 1);
             HIP_TRY(timed(d, LDPC_K_CN, s, [&] { return ldpc::launch_cn(G, st, par, s, true); }));
             HIP_TRY(ldpc::launch_cn_rare(G, st, par, s, true));
-            HIP_TRY(timed(d, LDPC_K_VN, s, [&] { return ldpc::launch_vn(G, st, 0, max_iter, nllr, s, ctr); }));
+            if (tail_ok && cur <= kTailTiles)
+                HIP_TRY(timed(d, LDPC_K_VN, s,
+                              [&] { return ldpc::launch_vn_tail(G, st, max_iter, nllr, d->tzb, d->tcnt, ctr, s); }));
+            else
+                HIP_TRY(timed(d, LDPC_K_VN, s, [&] { return ldpc::launch_vn(G, st, 0, max_iter, nllr, s, ctr); }));
             HIP_TRY(refill());
         }
         unsigned long long finished = 0, handed = 0;
@@ -803,7 +864,6 @@ int mc_stream_point(ldpc_decoder *d, uint64_t seed, int p, double sigma, int64_t
         const int64_t live = std::min<int64_t>((int64_t)handed, total) - (int64_t)finished;
         if (compact && (int64_t)handed >= total && cur > 1 && live > 0 && live * 2 <= (int64_t)cur * kTile) {
             const int nt = (int)((live + kTile - 1) / kTile);
-            const int cap = d->cap_tiles * kTile;
             if (!d->cpairs && dev_alloc(&d->cpairs, 1 + 2 * (size_t)cap)) return LDPC_ENOMEM;
             HIP_TRY(ldpc::launch_compact(G, st, nt, cap, d->cpairs, s));
             state_bind(d, nt, nt * kTile);

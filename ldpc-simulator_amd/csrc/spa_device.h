@@ -92,16 +92,25 @@ int tile_trace_read(unsigned long long *out, size_t n);  // LDPC_TILE_TRACE buil
 // Streaming Monte-Carlo through the tile-resident decoder (one launch per SNR
 // point; LDPC_TILE_STREAM=0 keeps the split CN/VN/refill loop).
 bool use_tile_stream(const DevGraph &g);
+// handoff > 0 (sub-tile decoder only): the kernel stops once the supply is
+// out and at most `handoff` frames still run, leaving them as split-path
+// slot state (done / iters / fresh; E, L, ch, ubits in place)
 hipError_t launch_tile_stream(const DevGraph &g, const DevState &st, int max_iter, bool nllr, uint64_t seed,
                               int snr_point, double sigma, int64_t frame0, int64_t total, unsigned long long *next,
-                              unsigned long long *ctr, hipStream_t s);
+                              unsigned long long *ctr, int64_t handoff, hipStream_t s);
 int sub_frames(const DevGraph &g);
 size_t sub_lds_bytes(const DevGraph &g);
 hipError_t launch_tile_sub(const DevGraph &g, const DevState &st, int max_iter, bool nllr, hipStream_t s);
 hipError_t launch_tile_sub_stream(const DevGraph &g, const DevState &st, int max_iter, bool nllr, uint64_t seed,
                                   int snr_point, double sigma, int64_t frame0, int64_t total,
-                                  unsigned long long *next, unsigned long long *ctr, hipStream_t s);
+                                  unsigned long long *next, unsigned long long *ctr, int64_t handoff, hipStream_t s);
 hipError_t launch_stream_init(const DevGraph &g, const DevState &st, hipStream_t s);
+// streaming tail (few tiles): column-parallel VN + per-tile syndrome/exits,
+// the same frames' results and counters as launch_vn(stream).  zb
+// [cap_tiles][ceil(n/32)][64] u32 and cnt [cap_tiles*64] int, all zero on entry
+// (left zero on exit); std_form graphs with k <= 2048
+hipError_t launch_vn_tail(const DevGraph &g, const DevState &st, int max_iter, bool nllr, uint32_t *zb, int *cnt,
+                          unsigned long long *ctr, hipStream_t s);
 hipError_t launch_refill(const DevGraph &g, const DevState &st, uint64_t seed, int snr_point, double sigma,
                          int64_t frame0, int64_t total, unsigned long long *next, hipStream_t s);
 // streaming tail: move the frames running in tiles >= nt into finished slots

@@ -492,6 +492,135 @@ __global__ __launch_bounds__(1024) void vn_kernel(DevGraph g, DevState st, int i
     }
 }
 
+// ----------------------------------------- streaming tail: column-parallel VN
+// vn_kernel runs one workgroup per tile, so with a handful of tiles left (the
+// drain of the streaming schedule) an iteration costs ~11 ms of one CU's
+// latency (profiles/r2au_tail).  The tail pair spreads a tile's columns over
+// the chip instead: vn_cols_kernel, one wavefront per (tile, column) -- the
+// column sum in rows-ascending CSC order (:173-185, scipy csr_matvec's order,
+// loads kept kTv deep ahead of the sequential adds), L, the normalized-LLR
+// count (:210-228) and the z^1 bit OR-ed into zb [tile][nw][64]; then
+// tail_exit_kernel, one workgroup per tile: the syndrome (:191-204) as
+// popcount(A_r & (z^1)_A) + (z^1)_{k+r} from the bit-packed rows, and exactly
+// vn_kernel<.., kStream>'s per-frame exits and counters (main.py:130-138).
+// zb and cnt are all-zero between iterations (tail_exit clears its tile).
+constexpr int kTv = 16;
+__global__ __launch_bounds__(256) void vn_cols_kernel(DevGraph g, DevState st, int nllr, uint32_t *zb, int *cnt) {
+    const int tile = blockIdx.y;
+    const int j = blockIdx.x * 4 + (int)(threadIdx.x >> 6);  // column (uniform per wavefront)
+    if (j >= g.n || !st.tile_active[tile]) return;
+    const int lane = threadIdx.x & 63;
+    const int f = tile * kTile + lane;
+    const bool live = st.done[f] == 0;
+    const double *Et = st.E + (size_t)tile * g.nnz * kTile + lane;
+    const int p0 = g.csc_ptr[j], p1 = g.csc_ptr[j + 1];
+    double s = 0.0;  // rows ascending, starting at 0.0
+    double ring[kTv];
+#pragma unroll
+    for (int q = 0; q < kTv; ++q) ring[q] = Et[(size_t)g.csc_edge[min(p0 + q, p1 - 1)] * kTile];
+    for (int p = p0; p < p1; p += kTv) {
+#pragma unroll
+        for (int q = 0; q < kTv; ++q) {
+            const double v = ring[q];
+            ring[q] = Et[(size_t)g.csc_edge[min(p + q + kTv, p1 - 1)] * kTile];
+            if (p + q < p1) s = s + v;
+        }
+    }
+    const size_t ci = ((size_t)tile * g.n + j) * kTile + lane;
+    const double chj = st.ch[ci];
+    const double Lj = chj + s;  // channel added after the sum
+    if (nllr && j < g.k) {
+        const double ap = st.L[ci];  // previous posterior (= ch on a frame's first pass)
+        if (fabs(Lj) <= 7.0 && ap * Lj < 0.0) atomicAdd(&cnt[f], 1);
+    }
+    if (live) st.L[ci] = Lj;
+    if (!(Lj < 0.0)) {
+        const int nw = (g.n + 31) >> 5;
+        atomicOr(&zb[((size_t)tile * nw + (j >> 5)) * kTile + lane], 1u << (j & 31));
+    }
+}
+
+constexpr int kTailWaves = 16;
+constexpr int kTailKw = 64;  // (z^1)_A words held per lane: k <= 2048
+__global__ __launch_bounds__(64 * kTailWaves) void tail_exit_kernel(DevGraph g, DevState st, int last, int nllr,
+                                                                     uint32_t *zb, int *cnt,
+                                                                     unsigned long long *ctr) {
+    __shared__ int bad[kTile];
+    const int tile = blockIdx.x;
+    if (!st.tile_active[tile]) return;  // block-uniform
+    const int lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6;
+    const int f = tile * kTile + lane;
+    const int kw = (g.k + 31) >> 5, nw = (g.n + 31) >> 5;
+    uint32_t *zt = zb + (size_t)tile * nw * kTile + lane;
+    if (threadIdx.x < kTile) bad[threadIdx.x] = 0;
+    __syncthreads();
+    uint32_t za[kTailKw];
+#pragma unroll
+    for (int w = 0; w < kTailKw; ++w) {
+        uint32_t v = w < kw ? zt[w * kTile] : 0u;
+        if (w == kw - 1 && (g.k & 31)) v &= (1u << (g.k & 31)) - 1u;  // A columns only
+        za[w] = v;
+    }
+    uint32_t acc = 0u;
+    for (int r = wave; r < g.m; r += kTailWaves) {
+        const uint32_t *ar = g.a_packed + (size_t)r * kw;
+        const int q = g.k + r;  // identity column of row r
+        uint32_t par = zt[(q >> 5) * kTile] >> (q & 31);
+#pragma unroll
+        for (int w = 0; w < kTailKw; ++w)
+            if (w < kw) par += __builtin_popcount(ar[w] & za[w]);
+        acc |= par & 1u;
+    }
+    if (acc) atomicOr(&bad[lane], 1);
+    __syncthreads();
+    if (wave == 0) {  // vn_kernel<false, true>'s exits and counters
+        const bool live = st.done[f] == 0;
+        const int itl = st.iters[f];
+        const bool lastl = itl == last - 1;
+        unsigned long long v[7] = {0, 0, 0, 0, 0, 0, 0};
+        bool fin = false, still = false;
+        if (live) {
+            const bool ok = bad[lane] == 0;
+            fin = ok || lastl;
+            if (fin) {
+                unsigned long long err = 0;
+                if (!ok) {  // u vs z^1 of the info columns (main.py:130-138)
+                    const uint32_t *Ut = st.ubits + (size_t)tile * kw * kTile + lane;
+#pragma unroll
+                    for (int w = 0; w < kTailKw; ++w)
+                        if (w < kw) err += __builtin_popcount(Ut[w * kTile] ^ za[w]);
+                }
+                v[0] = 1;
+                v[1] = ok ? 0 : 1;
+                v[2] = ok ? 0 : err;
+                v[3] = ok ? (unsigned long long)itl : 0;
+                v[4] = ok ? 1 : 0;
+                v[5] = nllr ? (unsigned long long)cnt[f] : 0;
+                v[6] = (unsigned long long)(itl + 1);
+                st.done[f] = 1;
+                st.refill[f] = 1;
+            } else {
+                st.iters[f] = itl + 1;
+                still = true;
+            }
+            st.fresh[f] = 0;
+        }
+        if (__ballot(fin) != 0ull) {
+#pragma unroll
+            for (int i = 0; i < 7; ++i) {
+                const unsigned long long sm = wave_sum(v[i]);
+                if (lane == 0 && sm) atomicAdd(&ctr[i], sm);
+            }
+        }
+        const unsigned long long any = __ballot(still);
+        if (lane == 0) st.tile_active[tile] = any != 0ull ? 1 : 0;
+        cnt[f] = 0;
+    }
+    __syncthreads();  // every wave has read zt
+    for (int w = wave; w < nw; w += kTailWaves) zt[w * kTile] = 0u;
+}
+
 // ------------------------------------------------------------ plumbing kernels
 __global__ void reset_kernel(DevState st) {
     const int f = blockIdx.x * blockDim.x + threadIdx.x;
@@ -717,6 +846,14 @@ hipError_t launch_vn(const DevGraph &g, const DevState &st, int it, int max_iter
     else
         vn_kernel<false, false><<<st.ntiles, kVnWaves * 64, lds, s>>>(g, st, it, last, nl, g.csc_ptr, g.csc_edge,
                                                                        g.csc_row, nullptr);
+    return hipGetLastError();
+}
+
+hipError_t launch_vn_tail(const DevGraph &g, const DevState &st, int max_iter, bool nllr, uint32_t *zb, int *cnt,
+                          unsigned long long *ctr, hipStream_t s) {
+    if (!g.a_packed || !st.ubits || ((g.k + 31) >> 5) > kTailKw) return hipErrorInvalidValue;
+    vn_cols_kernel<<<dim3((unsigned)((g.n + 3) / 4), (unsigned)st.ntiles), 256, 0, s>>>(g, st, nllr ? 1 : 0, zb, cnt);
+    tail_exit_kernel<<<st.ntiles, 64 * kTailWaves, 0, s>>>(g, st, max_iter, nllr ? 1 : 0, zb, cnt, ctr);
     return hipGetLastError();
 }
 

@@ -722,10 +722,11 @@ bool use_tile_stream(const DevGraph &g) {
 
 hipError_t launch_tile_stream(const DevGraph &g, const DevState &st, int max_iter, bool nllr, uint64_t seed,
                               int snr_point, double sigma, int64_t frame0, int64_t total, unsigned long long *next,
-                              unsigned long long *ctr, hipStream_t s) {
+                              unsigned long long *ctr, int64_t handoff, hipStream_t s) {
     const size_t lds = tile64_lds_bytes(g);
     if (!lds && sub16(g))
-        return launch_tile_sub_stream(g, st, max_iter, nllr, seed, snr_point, sigma, frame0, total, next, ctr, s);
+        return launch_tile_sub_stream(g, st, max_iter, nllr, seed, snr_point, sigma, frame0, total, next, ctr,
+                                      handoff, s);
     if (!lds || !g.a_packed || !st.ubits || st.ntiles > st.nslots) return hipErrorInvalidValue;
     tile_stream_kernel<<<st.ntiles, 64 * kTW, lds, s>>>(g, st, max_iter, nllr ? 1 : 0, g.col_idx, g.row_ptr,
                                                         kAtanhCoef, seed, snr_point, sigma, frame0, total, next, ctr);

@@ -221,6 +221,8 @@ template <int Q>
 __device__ __forceinline__ uint32_t sub_eoff(const SubCtx<Q> &c, const SubChunk &rc) {
     return ((uint32_t)(rc.c0 + c.j * rc.CS) << 9) + c.lo8;
 }
+// a lane's slot i of a row chunk is at most (Q-1)*CS + K - 1 < Q*K edges past the row's end
+static_assert(4 * SubCfg<4>::K <= kEPadEdges && 8 * SubCfg<8>::K <= kEPadEdges, "E slack too small");
 template <int Q>
 __device__ __forceinline__ double *sub_es(const SubCtx<Q> &c, uint32_t off, int i) {
     return (double *)(c.Eu + (size_t)off + (size_t)i * (kTile * sizeof(double)));
@@ -723,7 +725,7 @@ template <int Q>
 __global__ __launch_bounds__(64 * kSW, 1) void tile_sub_stream_kernel(
     DevGraph g, DevState st, int max_iter, int nllr, const int *__restrict__ col_idx,
     const int *__restrict__ row_ptr, AtanhCoef ac, uint64_t seed, int snr_point, double sigma, int64_t frame0,
-    int64_t total, unsigned long long *next, unsigned long long *ctr) {
+    int64_t total, unsigned long long *next, unsigned long long *ctr, int64_t handoff) {
     constexpr int F = SubCfg<Q>::F, K = SubCfg<Q>::K;
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     __shared__ int itl[F], freshl[F];
@@ -798,6 +800,18 @@ __global__ __launch_bounds__(64 * kSW, 1) void tile_sub_stream_kernel(
 
     for (int pass = 0;; ++pass) {
         if (wave == 0) {  // refill: slots without a frame take the next indices and generate them
+            // hand-off: once the supply is out and at most `handoff` frames
+            // are still running anywhere, stop here and leave them to the
+            // column-parallel tail (ldpc_api.cpp mc_stream_point): a running
+            // frame costs this workgroup a full pass per iteration
+            int stop = 0;
+            if (handoff > 0 && lane == 0) {
+                const long long nx = (long long)__hip_atomic_load(next, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                const long long fin = (long long)__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                stop = nx >= total && total - fin <= handoff ? 1 : 0;
+            }
+            stop = uniform(stop);
+            if (stop) want = false;
             const unsigned long long w = __ballot(want);
             if (w != 0ull) {
                 const int first = __ffsll((long long)w) - 1;
@@ -816,7 +830,15 @@ __global__ __launch_bounds__(64 * kSW, 1) void tile_sub_stream_kernel(
             }
             want = false;
             const unsigned long long any = __ballot(slot_lane && livel[f] != 0);
-            if (lane == 0) flags[2 * kSR + 1] = any != 0ull ? 1 : 0;
+            const bool go = any != 0ull && !stop;
+            if (!go && slot_lane) {  // the slots' state, in the split path's terms
+                const int fr = tile * kTile + lane64;
+                st.done[fr] = livel[f] != 0 ? 0 : 1;
+                st.iters[fr] = itl[f];
+                st.fresh[fr] = freshl[f];
+                st.refill[fr] = 0;
+            }
+            if (lane == 0) flags[2 * kSR + 1] = go ? 1 : 0;
         }
         __syncthreads();
         if (!flags[2 * kSR + 1]) break;  // supply exhausted, every slot drained
@@ -930,14 +952,14 @@ size_t sub_lds_bytes(const DevGraph &g) {
 
 hipError_t launch_tile_sub_stream(const DevGraph &g, const DevState &st, int max_iter, bool nllr, uint64_t seed,
                                   int snr_point, double sigma, int64_t frame0, int64_t total,
-                                  unsigned long long *next, unsigned long long *ctr, hipStream_t s) {
+                                  unsigned long long *next, unsigned long long *ctr, int64_t handoff, hipStream_t s) {
     const size_t lds = sub_lds_bytes_q<4>(g);
     // the 16-frame form only (+ 2 x 16 ints of static LDS per-slot state)
     if (!lds || !g.a_packed || !st.ubits || st.ntiles > st.nslots || lds + 2 * 16 * sizeof(int) > kSubLdsMax)
         return hipErrorInvalidValue;
     tile_sub_stream_kernel<4><<<st.ntiles * 4, 64 * kSW, lds, s>>>(g, st, max_iter, nllr ? 1 : 0, g.col_idx, g.row_ptr,
                                                                    kAtanhCoef, seed, snr_point, sigma, frame0, total,
-                                                                   next, ctr);
+                                                                   next, ctr, handoff);
     return hipGetLastError();
 }
 

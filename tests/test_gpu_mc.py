@@ -145,7 +145,8 @@ def test_stream_zero_frames(gpu_available):
     ("wimax_2304_0.5", 256, 700, 12, (1.0, 3.0)),   # 16-frame sub-tiles (tile_sub_stream_kernel)
     ("wimax_2304_0.5", 64, 150, 1, (2.0,)),         # sub-tiles, max_iter 1
 ])
-def test_tile_stream_equals_split_stream(gpu_available, code, cap, frames, T, snrs):
+def test_tile_stream_equals_split_stream(gpu_available, code, cap, frames, T, snrs, monkeypatch):
+    monkeypatch.setenv("LDPC_HANDOFF", "0")  # the whole point in the tile kernel (hand-off: next test)
     dec = _decoder(code, cap)
     sig = [oracle.sigma_for_snr(s) for s in snrs]
     dec.profile(True)
@@ -188,3 +189,30 @@ def test_fit_slots_caps_the_workspace(gpu_available):
     dec = Decoder(g, slots)
     ctr = dec.mc_run(SEED, [oracle.sigma_for_snr(3.0)], 3 * slots + 5, 0, 6)
     assert ctr[0, 0] == 3 * slots + 5
+
+
+@pytest.mark.parametrize("handoff", ["256", "20"])
+def test_stream_handoff_keeps_counters(gpu_available, monkeypatch, handoff):
+    """The streaming sub-tile kernel hands its last running frames to the split
+    path's column-parallel tail (launch_vn_tail) once the supply is out: the
+    counters equal the sub-tile kernel draining alone, the static schedule and
+    the split stream with the per-tile vn_kernel."""
+    code, cap, frames, T = "wimax_2304_0.5", 256, 1500, 20
+    dec = _decoder(code, cap)
+    sig = [oracle.sigma_for_snr(s) for s in (2.5, 3.0)]
+    monkeypatch.setenv("LDPC_HANDOFF", handoff)
+    dec.profile(True)
+    a = dec.mc_run(SEED, sig, frames, 11, T, nllr=True)
+    p = dec.profile_read()
+    dec.profile(False)
+    assert p["tile"][1] == 2 and p["cn"][1] > 0, p  # the tail ran on the split path
+    monkeypatch.setenv("LDPC_HANDOFF", "0")
+    b = dec.mc_run(SEED, sig, frames, 11, T, nllr=True)
+    c = dec.mc_run(SEED, sig, frames, 11, T, nllr=True, static=True)
+    monkeypatch.setenv("LDPC_TAIL_VN", "0")
+    d = dec.mc_run(SEED, sig, frames, 11, T, nllr=True, split=True)
+    monkeypatch.delenv("LDPC_TAIL_VN")
+    e = dec.mc_run(SEED, sig, frames, 11, T, nllr=True, split=True)
+    for x in (b, c, d, e):
+        np.testing.assert_array_equal(a, x)
+    assert (a[:, 0] == frames).all()

@@ -7,7 +7,7 @@ O=gpurun_out/${TAG:-ab}; mkdir -p $O
 for round in 1 2; do
   for name in "$@"; do
     lib=variants/$name.so
-    for cfg in s1 t2a t2b; do
+    for cfg in ${CFGS:-s1 t2a t2b}; do
       case $cfg in
         s1) A="--frames 16384 --steps 1 --warmup 1";;
         t2a) A="--snr 2.0 --schedule stream --chunk 8192 --frames 32768 --steps 1 --warmup 0";;
