@@ -209,11 +209,12 @@ __global__ __launch_bounds__(256, LDPC_CN_WAVES) void cn_kernel(DevGraph g, DevS
 constexpr int kRowW = 8, kRowK = 24;
 // S: phase-1 load stages (K/S edges' loads in flight per stage); WPS: min
 // wavefronts per SIMD (register cap 512/WPS).
-template <bool kFirst, bool kStream, int S, int WPS>
-__global__ __launch_bounds__(64 * kRowW, WPS) void cn_row_kernel(DevGraph g, DevState st, int it_parity,
-                                                                 const int *__restrict__ col_idx,
-                                                                 const int *__restrict__ row_ptr, AtanhCoef ac) {
-    constexpr int W = kRowW, K = kRowK;
+// W, K: a second shape, 16 wavefronts x 40 edges (rows <= 640: wimax_2304_0.5,
+// 416-632), serves the 2304 code's split path and its streaming tail.
+template <bool kFirst, bool kStream, int S, int WPS, int W = kRowW, int K = kRowK>
+__global__ __launch_bounds__(64 * W, WPS) void cn_row_kernel(DevGraph g, DevState st, int it_parity,
+                                                             const int *__restrict__ col_idx,
+                                                             const int *__restrict__ row_ptr, AtanhCoef ac) {
     __shared__ MathLds mlds;
     __shared__ double chain[kTile];  // running product handed from wavefront to wavefront
     fill_math_lds(mlds);
@@ -790,15 +791,32 @@ bool use_cn_row(const DevGraph &g) {
     return force != 0 && g.max_row_deg <= kRowW * kRowK;
 }
 
+// 16 x 40 shape for rows of 193..640 edges, from 64 tiles on: on a full chunk
+// of wimax_2304_0.5 (128 tiles) its CN pass is 10 % faster than cn_kernel's
+// (16 B instead of 24 B per edge, one tanh per edge instead of two); in the
+// few-tile streaming tail, where one 16-wavefront workgroup per CU is all
+// that fits, 1.5 % slower (profiles/r2aw_cn_row16).  LDPC_CN_ROW16 (read per
+// call): 0 = never, 1 = at any tile count, unset = from 64 tiles.
+constexpr int kRow16W = 16, kRow16K = 40;
+bool use_cn_row16(const DevGraph &g, int ntiles) {
+    if (use_cn_row(g) || g.max_row_deg > kRow16W * kRow16K) return false;
+    const char *e = getenv("LDPC_CN_ROW16");
+    return e ? atoi(e) != 0 : ntiles >= 64;
+}
+
 template <bool kFirst, bool kStream>
 void launch_cn_row(const DevGraph &g, const DevState &st, int par, hipStream_t s) {
     const unsigned grid = (unsigned)(((st.ntiles + 7) / 8) * 8 * g.m);
     const int *ci = g.col_idx, *rp = g.row_ptr;
-    cn_row_kernel<kFirst, kStream, 4, 6><<<grid, 64 * kRowW, 0, s>>>(g, st, par, ci, rp, kAtanhCoef);
+    if (use_cn_row(g))
+        cn_row_kernel<kFirst, kStream, 4, 6><<<grid, 64 * kRowW, 0, s>>>(g, st, par, ci, rp, kAtanhCoef);
+    else
+        cn_row_kernel<kFirst, kStream, 4, 4, kRow16W, kRow16K><<<grid, 64 * kRow16W, 0, s>>>(g, st, par, ci, rp,
+                                                                                            kAtanhCoef);
 }
 
 hipError_t launch_cn(const DevGraph &g, const DevState &st, int it, hipStream_t s, bool stream) {
-    if (use_cn_row(g)) {
+    if (use_cn_row(g) || use_cn_row16(g, st.ntiles)) {
         const int par = it & 1;
         if (stream)
             launch_cn_row<false, true>(g, st, par, s);

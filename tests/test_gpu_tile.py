@@ -145,3 +145,17 @@ def test_sub_tile_rare_rows_identical(gpu_available, sub_tile):
     for T in (1, 3):
         _assert_identical(dec.decode(llr, T, nllr=True, post=True, msgs=True),
                           dec.decode(llr, T, nllr=True, post=True, msgs=True, split=True))
+
+
+@pytest.mark.parametrize("snr,T,B", [(0.0, 4, 70), (3.0, 25, 40)])
+def test_cn_row16_bit_identical_to_sub_tile(gpu_available, monkeypatch, snr, T, B):
+    """The 16-wavefront x 40-edge cn_row_kernel shape (rows of wimax_2304_0.5;
+    by default only from 64 tiles on, forced here) == the sub-tile decoder."""
+    code = "wimax_2304_0.5"
+    llr = _random_llr(hstd_for(code), B, snr, seed=int(100 * snr) + 3000 + T)
+    llr[1, ::5] = 0.0  # a rare row (|t| <= 1e-10) for cn_rare_kernel
+    dec = _decoder(code, B)
+    a = dec.decode(llr, T, nllr=True, post=True, hist=True, msgs=True)
+    monkeypatch.setenv("LDPC_CN_ROW16", "1")
+    b = dec.decode(llr, T, nllr=True, post=True, hist=True, msgs=True, split=True)
+    _assert_identical(a, b)
