@@ -12,9 +12,18 @@ frames on the GPU (info bits -> [u, A.u] -> BPSK -> AWGN -> LLR), decode them
 (up to 50 iterations with early termination) and reduce the main.py counters
 on the device.  With N GPUs (one process per GPU, launched by
 torch.distributed.run) every rank decodes its own disjoint frame range and the
-counters are summed with ONE all-reduce (weak scaling).  After the timed
-region, one step each at --extra-snr points (default 2.0 and 3.0 dB) is timed
-and reported under "snr_points".
+counters are summed with ONE all-reduce over RCCL (weak scaling).  After the
+timed region, one step each at --extra-snr points (default 2.0 and 3.0 dB) is
+timed and reported under "snr_points", and a few steps of the physical mode
+(the north-star's absolute cw/s target, NOT the
+reference's arithmetic) under "physical".
+
+Launch: under torch.distributed.run (RANK / WORLD_SIZE set) every process is
+one rank.  `bench.py --gpus N` (N > 1) with no launcher around it starts its
+own N rank processes (self_launch: fresh children, before anything touches
+HIP) -- as the reference's main.py starts its own worker pool
+(python_ldpc_app/main.py:248-291).  `n_gpus` in the JSON line is the number of
+ranks that answered on the communicator (`ranks_seen`), never the flag.
 
 Output: ONE JSON line on rank 0 (contract in the task statement), with
 `roofline` for the whole decode (algorithmic bytes, SURVEY.md section 8d, over
@@ -67,12 +76,74 @@ def parse():
                          "SURVEY §8 f4, standard SPA on the sparse graph, fp32, LDS-resident")
     ap.add_argument("--phys-hbm", action="store_true",
                     help="physical mode: HBM-resident state even when a frame fits in LDS")
-    ap.add_argument("--comm", choices=("rccl", "torch"), default="rccl",
-                    help="N>1 exchange: rccl = RCCL through the C ABI (ldpc_amd.comm, no PyTorch); "
-                         "torch = torch.distributed with --dist-backend")
-    ap.add_argument("--dist-backend", default="nccl",
-                    help="--comm torch only: 'nccl' (= RCCL) or 'gloo' (rehearse several ranks on one GPU)")
+    ap.add_argument("--phys-steps", type=int, default=4,
+                    help="parity mode: timed physical-mode steps reported under 'physical' after the "
+                         "headline (0 = none); not the reference's arithmetic (SURVEY 8 f4)")
+    ap.add_argument("--phys-frames", type=int, default=65536, help="frames per physical-mode step")
+    ap.add_argument("--stub", action="store_true",
+                    help="launcher rehearsal without a GPU: every rank only joins a gloo group and "
+                         "counts the ranks (tests/test_bench_launch.py); also LDPC_BENCH_STUB=1")
     return ap.parse_args()
+
+
+def self_launch(args, argv):
+    """`bench.py --gpus N` (N > 1) with no launcher around it: start N fresh
+    child processes of this script, rank r on GPU r, each with RANK /
+    LOCAL_RANK / WORLD_SIZE / MASTER_ADDR / MASTER_PORT and one rendezvous key
+    for the whole launch (LDPC_RDV_KEY, ldpc_amd.comm).  Runs before anything
+    imports ldpc_amd or touches HIP, and starts the children with subprocess
+    (never exec).  Rank 0's stdout (the JSON line) is ours; the other ranks'
+    stdout is discarded.  If a rank fails, the others are stopped and the
+    launch exits non-zero.  -> exit status."""
+    import signal
+    import socket
+    import subprocess
+    import uuid
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    key = uuid.uuid4().hex
+    procs = []
+    for r in range(args.gpus):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(args.gpus),
+                   LOCAL_WORLD_SIZE=str(args.gpus), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
+                   LDPC_RDV_KEY=key)
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv), env=env,
+                                      stdout=None if r == 0 else subprocess.DEVNULL))
+    status = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            rc = p.poll()
+            if rc is None:
+                continue
+            live.remove(p)
+            if rc != 0 and status == 0:
+                status = rc if rc > 0 else 128 - rc
+                print(f"bench.py: rank {procs.index(p)} exited with {rc}; stopping the other ranks",
+                      file=sys.stderr)
+                for q in live:  # the processes this launcher started, by their own handles
+                    q.send_signal(signal.SIGTERM)
+        time.sleep(0.05)
+    return status
+
+
+def stub_rank(args, world, rank):
+    """--stub: the launcher's contract without a GPU -- join a gloo group of
+    WORLD_SIZE ranks, count them, rank 0 prints the JSON line."""
+    import torch
+    import torch.distributed as dist
+    dist.init_process_group("gloo", init_method=f"tcp://{os.environ.get('MASTER_ADDR', '127.0.0.1')}:"
+                                                f"{os.environ.get('MASTER_PORT', '29500')}",
+                            rank=rank, world_size=world)
+    t = torch.ones(1, dtype=torch.int64)
+    dist.all_reduce(t)
+    seen = int(t.item())
+    if rank == 0:
+        print(json.dumps({"metric": METRIC, "value": None, "stub": True, "n_gpus": seen, "ranks_seen": seen,
+                          "world_size": world, "gpus_flag": args.gpus,
+                          "rdv_key_set": bool(os.environ.get("LDPC_RDV_KEY"))}), flush=True)
+    dist.destroy_process_group()
 
 
 class RcclDist:
@@ -93,41 +164,11 @@ class RcclDist:
     def barrier(self):
         self.c.barrier()  # all ranks arrive, then hipDeviceSynchronize
 
+    def ranks_seen(self):
+        return self.c.ranks_seen()
+
     def close(self):
         self.c.close()
-
-
-class TorchDist:
-    """--comm torch: the same exchange through torch.distributed (backend 'nccl'
-    = RCCL, or 'gloo' to rehearse several ranks on one GPU)."""
-
-    def __init__(self, device, backend):
-        import torch
-        import torch.distributed as dist
-        torch.cuda.set_device(device)
-        if backend == "nccl":  # bind the rank's GPU explicitly
-            dist.init_process_group("nccl", device_id=torch.device(f"cuda:{device}"))
-        else:
-            dist.init_process_group(backend)
-        self.torch, self.dist, self.device = torch, dist, device
-        self.dev = "cpu" if backend == "gloo" else f"cuda:{device}"
-
-    def allreduce(self, ctr):
-        t = self.torch.from_numpy(np.asarray(ctr, np.int64).reshape(-1).copy()).to(self.dev)
-        self.dist.all_reduce(t)
-        return t.cpu().numpy().reshape(np.shape(ctr))
-
-    def max(self, x):
-        t = self.torch.tensor([x], dtype=self.torch.float64, device=self.dev)
-        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
-        return float(t.item())
-
-    def barrier(self):
-        self.dist.barrier()
-        self.torch.cuda.synchronize(self.device)
-
-    def close(self):
-        self.dist.destroy_process_group()
 
 
 def dist_setup(args):
@@ -139,7 +180,7 @@ def dist_setup(args):
     # all-reduce, barriers, max over ranks) with a single rank -- how the
     # driver's multi-GPU run is rehearsed on a one-GPU box
     if world > 1 or os.environ.get("LDPC_BENCH_FORCE_DIST") == "1":
-        dist = RcclDist(local) if args.comm == "rccl" else TorchDist(local, args.dist_backend)
+        dist = RcclDist(local)
     return world, rank, local, dist
 
 
@@ -286,16 +327,88 @@ def cpu_baseline_phys(H, k, args, ira_code):
 IRA_CODES = {"dvbs2_profile_64800_0.5": "dvbs2_profile_matrix"}
 
 
+def physical_extra(args, edd, graph, local, world, rank, dist, k):
+    """The north-star's absolute target (>= 1e8 cw/s on wimax_2304_0.5 at 50
+    max iterations over 8 GPUs) is reachable only in physical mode (SURVEY 8d,
+    8 f4): standard SPA on the sparse graph H[:, perm], sign-consistent, fp32,
+    a frame's state in LDS.  NOT the reference's arithmetic (no parity): timed
+    here after the parity headline, outside its timed region, over the same
+    code, max_iter, SNR and on-device frame source, on frame indices disjoint
+    from the headline's.  Roofline = VALU issue (the state never leaves LDS):
+    committed PMC VALU instructions per frame-iteration of the same kernel and
+    code x this run's frame-iterations / the kernel's HIP-event time."""
+    from ldpc_amd import _lib
+    from ldpc_amd.device import Decoder, Graph
+    pg = Graph(edd.physical_matrix(), device=local)
+    B = args.phys_frames
+    pdec = Decoder(graph, B)  # frame source = H_std; E is never allocated in physical mode
+    sig = 1.0 / math.sqrt(2.0 * 1.0 * (10.0 ** (args.snr * 0.1)))
+    base = 1 << 42  # far from the parity steps' frame ranges
+    pdec.phys_mc_run(pg, SEED, [sig], B, base + rank * B, args.iters)  # untimed warm-up
+    barrier(dist, local)
+    pdec.profile_read()
+    pdec.profile(True)
+    barrier(dist, local)
+    t0 = time.perf_counter()
+    loc = np.zeros((1, 7), np.int64)
+    tot = np.zeros((1, 7), np.int64)
+    for s in range(args.phys_steps):
+        c = pdec.phys_mc_run(pg, SEED, [sig], B, base + ((s + 1) * world + rank) * B, args.iters)
+        loc += c
+        tot += allreduce_counters(dist, c, local)
+    barrier(dist, local)
+    dt = max_over_ranks(dist, time.perf_counter() - t0, local)
+    pdec.profile(False)
+    prof = pdec.profile_read()
+    pms, pl = prof["phys"]
+    name = _lib.lib().ldpc_phys_kernel_name(pg.handle, 0).decode()
+    frames = int(tot[0, 0])
+    out = {"what": "physical mode (SURVEY 8 f4): standard SPA on the sparse H[:,perm], sign-consistent, fp32, "
+                   "state in LDS -- NOT the reference's arithmetic, no parity with spa_decoder.py; timed after "
+                   "and outside the parity headline",
+           "value": frames / dt, "unit": "codewords/s", "per_gpu": frames / dt / world, "n_gpus": world,
+           "steps": args.phys_steps, "frames_per_gpu_step": B, "ms_per_step": dt / args.phys_steps * 1e3,
+           "info_bits_per_s": frames * k / dt, "dtype": "f32", "snr_db": args.snr, "max_iter": args.iters,
+           "edges_H_phys": int(pg.nnz), "fer": int(tot[0, 1]) / max(frames, 1),
+           "ber": int(tot[0, 2]) / (k * max(frames, 1)), "avg_iters": int(tot[0, 6]) / max(frames, 1),
+           "kernel": name, "kernel_ms": pms, "launches": pl,
+           "north_star_target_cw_s_8gpu": 1e8}
+    vi, vsrc = committed_valu(args.code, name)
+    if vi and pms:
+        ach = vi * int(loc[0, 6]) / (pms / 1e3)
+        out["roofline"] = {"bound": "valu", "achieved": ach, "peak": VALU_PEAK, "unit": "VALU wave-instr/s",
+                           "frac": ach / VALU_PEAK, "valu_insts_per_frame_iteration": vi, "valu_source": vsrc,
+                           "peak_model": "256 CUs x 4 SIMDs x 2.4 GHz / 2 cycles per wave64 fp32 VALU "
+                                         "instruction (MI355X_MICROARCH.md)"}
+    pdec.close()
+    return out
+
+
 def main():
     args = parse()
-    world, rank, local, dist = dist_setup(args)
-    if args.gpus != world and world > 1:
-        print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
+    launched = "WORLD_SIZE" in os.environ
+    if args.gpus < 1:
+        raise SystemExit("bench.py: --gpus must be >= 1")
+    if not launched and args.gpus > 1:
+        sys.exit(self_launch(args, sys.argv[1:]))  # nothing has touched HIP in this process
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but the launcher started WORLD_SIZE={world} ranks")
+    if args.stub or os.environ.get("LDPC_BENCH_STUB") == "1":
+        return stub_rank(args, world, int(os.environ.get("RANK", "0")))
     import ldpc_amd
     from ldpc_amd.device import Decoder, Graph
 
-    if ldpc_amd.device_count() <= 0:
+    ndev = ldpc_amd.device_count()
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if ndev <= 0:
         raise SystemExit("bench.py: no HIP device visible (the decoder has no CPU path)")
+    if local >= ndev:
+        raise SystemExit(f"bench.py: LOCAL_RANK {local} wants GPU {local} but only {ndev} are visible")
+    world, rank, local, dist = dist_setup(args)
+    ranks_seen = dist.ranks_seen() if dist is not None else 1
+    if ranks_seen != world:
+        raise SystemExit(f"bench.py: {ranks_seen} ranks answered on RCCL, WORLD_SIZE={world}")
     ira_code = args.code in IRA_CODES
     if ira_code:  # BASELINE config 5: sparse (physical) mode only, the IRA graph is its own frame source
         from ldpc_amd import ira
@@ -385,6 +498,11 @@ def main():
                            "avg_iters": int(c[0, 6]) / max(f, 1),
                            "fer": int(c[0, 1]) / max(f, 1), "ber": int(c[0, 2]) / (k * max(f, 1))})
 
+    physical = None
+    if args.phys_steps > 0 and pgraph is None and not ira_code:
+        dec.close()
+        physical = physical_extra(args, edd, graph, local, world, rank, dist, k)
+
     frames_total = int(totals[0, 0])
     assert frames_total == B * world * args.steps, (frames_total, B, world, args.steps)
     iters_total = int(totals[0, 6])  # whole job
@@ -420,7 +538,8 @@ def main():
         "value": cw_s,
         "unit": "codewords/s",
         "info_bits_per_s": cw_s * k,
-        "n_gpus": world,
+        "n_gpus": ranks_seen,
+        "ranks_seen": ranks_seen,
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": elapsed / args.steps * 1e3,
@@ -454,6 +573,8 @@ def main():
     }
     if snr_points:
         out["snr_points"] = snr_points
+    if physical is not None:
+        out["physical"] = physical
     if not tile_launches and pgraph is None and cn_launches:
         # separate CN / VN launches: the roofline is the WHOLE decode, one "launch" = one
         # CN + one VN sweep over the resident slots; traffic = PMC bytes of the same pair

@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define LDPC_ABI_VERSION 2
+#define LDPC_ABI_VERSION 3  /* 3: ldpc_diag_tile_trace removed */
 
 /* error codes */
 #define LDPC_OK 0
@@ -215,9 +215,6 @@ int ldpc_phys_mc_run(ldpc_decoder *d_std, const ldpc_graph *g_phys, uint64_t see
 #define LDPC_K_NKINDS 8
 int ldpc_profile_enable(ldpc_decoder *d, int enable);
 int ldpc_profile_read(ldpc_decoder *d, double *ms_out, int64_t *launches_out);
-/* Retired diagnostic (round 1's s_memtime phase trace of tile_kernel, a
- * separate build): kept for ABI stability, always returns -1. */
-int ldpc_diag_tile_trace(uint64_t *out, int64_t n);
 
 /* ------------------------------------------------ multi-GPU (RCCL, xGMI)
  * One process per GPU; frames are sharded by global index, so the only

@@ -96,7 +96,7 @@ int ldpc_comm_init(const uint8_t *id, int32_t rank, int32_t world, int32_t devic
         return ldpc_fail(LDPC_EDEVICE, "ldpc_comm_init: device %d not visible (%d devices)", device, ndev);
     const Rccl *r = rccl();
     if (!r) return LDPC_EDEVICE;
-    if (hipSetDevice(device) != hipSuccess) return ldpc_fail(LDPC_EDEVICE, "ldpc_comm_init: hipSetDevice failed");
+    DeviceGuard dg(device);  // the caller's current device is restored on return
     auto *c = new ldpc_comm;
     c->r = r;
     c->device = device;
@@ -124,7 +124,7 @@ int ldpc_comm_allreduce(ldpc_comm *c, void *buf, int64_t count, int32_t dtype, i
         (op != LDPC_OP_SUM && op != LDPC_OP_MAX))
         return ldpc_fail(LDPC_EINVAL, "ldpc_comm_allreduce: bad arguments");
     if (count == 0) return LDPC_OK;
-    if (hipSetDevice(c->device) != hipSuccess) return ldpc_fail(LDPC_EDEVICE, "hipSetDevice failed");
+    DeviceGuard dg(c->device);
     const ncclDataType_t dt = dtype == LDPC_DT_I64 ? ncclInt64 : ncclFloat64;
     const ncclRedOp_t ro = op == LDPC_OP_SUM ? ncclSum : ncclMax;
     const size_t bytes = (size_t)count * 8;
@@ -162,7 +162,7 @@ int ldpc_comm_barrier(ldpc_comm *c) {
 
 int ldpc_comm_destroy(ldpc_comm *c) {
     if (!c) return LDPC_OK;
-    (void)hipSetDevice(c->device);
+    DeviceGuard dg(c->device);
     if (c->comm) (void)c->r->destroy(c->comm);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     (void)hipFree(c->scratch);
@@ -171,7 +171,11 @@ int ldpc_comm_destroy(ldpc_comm *c) {
 }
 
 int ldpc_device_synchronize(int32_t device) {
-    if (hipSetDevice(device) != hipSuccess || hipDeviceSynchronize() != hipSuccess)
+    int ndev = 0;
+    if (device < 0 || hipGetDeviceCount(&ndev) != hipSuccess || device >= ndev)
+        return ldpc_fail(LDPC_EDEVICE, "ldpc_device_synchronize: device %d not visible", device);
+    DeviceGuard dg(device);
+    if (hipDeviceSynchronize() != hipSuccess)
         return ldpc_fail(LDPC_EDEVICE, "ldpc_device_synchronize(%d) failed", device);
     return LDPC_OK;
 }

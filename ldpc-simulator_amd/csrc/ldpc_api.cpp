@@ -86,17 +86,6 @@ struct ldpc_decoder {
 
 namespace {
 
-struct DeviceGuard {
-    int prev = -1;
-    explicit DeviceGuard(int dev) {
-        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
-        if (dev >= 0 && dev != prev) (void)hipSetDevice(dev);
-    }
-    ~DeviceGuard() {
-        if (prev >= 0) (void)hipSetDevice(prev);
-    }
-};
-
 // Sub-tile decoder's S order (tile_sub.hip sub_p3): wavefront w's P3 of row r
 // waits for row r-1's P3 by wavefronts [lo, hi], those whose chunk's extended
 // column span (from just past the previous non-empty chunk's last column to
@@ -787,9 +776,11 @@ int mc_stream_point(ldpc_decoder *d, uint64_t seed, int p, double sigma, int64_t
     const int cap = d->cap_tiles * kTile;
     // streaming tail VN (column-parallel, launch_vn_tail) once few tiles run
     const bool tail_ok = G.a_packed && ((G.k + 31) >> 5) <= 64 && tail_vn_enabled();
-    if (tail_ok && !d->tzb) {
+    if (tail_ok) {
         const size_t nzb = (size_t)d->cap_tiles * ((G.n + 31) / 32) * kTile;
-        if (dev_alloc(&d->tzb, nzb) || dev_alloc(&d->tcnt, (size_t)cap)) return LDPC_ENOMEM;
+        if (!d->tzb && (dev_alloc(&d->tzb, nzb) || dev_alloc(&d->tcnt, (size_t)cap))) return LDPC_ENOMEM;
+        // tail_exit_kernel leaves them zero, but a point that stopped early (an
+        // error return) may not have: cleared per point, never trusted
         HIP_TRY(hipMemsetAsync(d->tzb, 0, nzb * sizeof(uint32_t), s));
         HIP_TRY(hipMemsetAsync(d->tcnt, 0, (size_t)cap * sizeof(int), s));
     }
@@ -1153,11 +1144,6 @@ int ldpc_phys_mc_run(ldpc_decoder *d, const ldpc_graph *gp, uint64_t seed, int32
 }
 
 // -------------------------------------------------------------- profiling
-int ldpc_diag_tile_trace(uint64_t *out, int64_t n) {
-    if (!out || n <= 0) return ldpc_fail(LDPC_EINVAL, "ldpc_diag_tile_trace: no buffer");
-    return ldpc::tile_trace_read((unsigned long long *)out, (size_t)n);
-}
-
 int ldpc_profile_enable(ldpc_decoder *d, int enable) {
     if (!d) return ldpc_fail(LDPC_EINVAL, "ldpc_profile_enable: NULL decoder");
     d->prof = enable != 0;

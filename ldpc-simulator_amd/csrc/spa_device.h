@@ -88,7 +88,6 @@ size_t tile_lds_bytes(const DevGraph &g);
 const char *tile_kernel_name(const DevGraph &g);  // "tile_kernel", "tile_sub_kernel" or ""
 bool use_tile(const DevGraph &g);
 hipError_t launch_tile(const DevGraph &g, const DevState &st, int max_iter, bool nllr, hipStream_t s);
-int tile_trace_read(unsigned long long *out, size_t n);  // LDPC_TILE_TRACE builds
 // Streaming Monte-Carlo through the tile-resident decoder (one launch per SNR
 // point; LDPC_TILE_STREAM=0 keeps the split CN/VN/refill loop).
 bool use_tile_stream(const DevGraph &g);

@@ -656,14 +656,6 @@ __global__ __launch_bounds__(64 * kTW, 1) void tile_stream_kernel(DevGraph g, De
 
 }  // namespace
 
-// The phase-trace diagnostic build (s_memtime stamps) was retired with the
-// other A/B switches (round 2); the ABI entry reports that.
-int tile_trace_read(unsigned long long *out, size_t n) {
-    (void)out;
-    (void)n;
-    return -1;
-}
-
 size_t tile64_lds_bytes(const DevGraph &g) {
     if (!g.std_form || !g.a_packed || g.k <= 0 || g.k > 32 * kTKW || g.max_row_deg > kTW * kTK) return 0;
     const size_t b = tile_layout(g.k, g.m).total;

@@ -536,19 +536,30 @@ __device__ __forceinline__ void sub_p3_body(SubCtx<Q> &c, int r, double (&t)[Sub
 // the host: ldpc_api.cpp sub_p3_deps) orders every column's additions by
 // induction over the rows -- the neighbours, not all 16 wavefronts (the full
 // row barrier this replaces cost early wavefronts up to 39 % of their time,
-// profiles/r2an_phase_timers).  p3row[v] = 1 + the last global row (pass*m + r)
-// whose P3 wavefront v finished; passes are separated by __syncthreads.
+// profiles/r2an_phase_timers).  p3row[v] = 1 + the last row r of THIS pass
+// whose P3 wavefront v finished; sub_p3_reset zeroes it between passes (after
+// the barrier that ends a pass's rows), so the count never exceeds m + 1 however
+// many passes a streaming launch makes.
 template <int Q, int BF>
 __device__ __forceinline__ void sub_p3(SubCtx<Q> &c, int r, double (&t)[SubCfg<Q>::K]) {
-    const int g = c.ep0 + r;
     if (r > 0) {  // row r-1's P3 by the wavefronts whose column spans overlap ours
         const int d = c.p3dep[r * kSW + c.wave];
-        for (int v = d & 0xff; v <= (d >> 8); ++v) wait_ge<false>(c.p3row + v, g);
+        for (int v = d & 0xff; v <= (d >> 8); ++v) wait_ge<false>(c.p3row + v, r);
     }
     sub_p3_body<Q, BF>(c, r, t);
     lds_release();  // this row's S additions before the count
     if ((threadIdx.x & 63) == 0)
-        lds_st(c.p3row + c.wave, g + 1);
+        lds_st(c.p3row + c.wave, r + 1);
+}
+// Between passes: every wavefront has finished (and waited on) the pass's
+// P3s -- call after the barrier that ends the row loop, before the next one.
+__device__ __forceinline__ void sub_p3_reset(int *p3row) {
+    if (threadIdx.x < kSW) p3row[threadIdx.x] = 0;
+}
+// Chain-flag epoch of a pass: (pass * m) mod 2^26, so ep0 + r (masked again
+// where used) neither overflows nor breaks the sequence of epochs across passes.
+__device__ __forceinline__ int sub_epoch0(int pass, int m) {
+    return (int)(((uint32_t)pass * (uint32_t)m) & 0x3ffffffu);
 }
 
 template <int Q, int BF>
@@ -631,7 +642,7 @@ __global__ __launch_bounds__(64 * kSW, 1) void tile_sub_kernel(DevGraph g, DevSt
     for (int it = 0; it < max_iter; ++it) {
         c.first = it == 0;
         c.live = livel[f] != 0;
-        c.ep0 = it * m;
+        c.ep0 = sub_epoch0(it, m);
         double tA[K], tB[K];
         bool yA = false, yB = false;
         if (m > 0) {
@@ -643,6 +654,7 @@ __global__ __launch_bounds__(64 * kSW, 1) void tile_sub_kernel(DevGraph g, DevSt
             if (r + 1 <= m) sub_body<Q, kStaticBF>(c, r + 1, m, tB, yB, tA, yA);
         }
         __syncthreads();  // every P3 done: S complete, identity bits set
+        sub_p3_reset(c.p3row);
 
         // posteriors of the A columns (channel added after the sum), the
         // normalized-LLR count against the previous posterior (:210-228),
@@ -844,7 +856,7 @@ __global__ __launch_bounds__(64 * kSW, 1) void tile_sub_stream_kernel(
         if (!flags[2 * kSR + 1]) break;  // supply exhausted, every slot drained
         c.live = livel[f] != 0;
         c.fresh = freshl[f] != 0;
-        c.ep0 = pass * m;
+        c.ep0 = sub_epoch0(pass, m);
         double tA[K], tB[K];
         bool yA = false, yB = false;
         if (m > 0) {
@@ -856,6 +868,7 @@ __global__ __launch_bounds__(64 * kSW, 1) void tile_sub_stream_kernel(
             if (r + 1 <= m) sub_body<Q, kStreamBF>(c, r + 1, m, tB, yB, tA, yA);
         }
         __syncthreads();
+        sub_p3_reset(c.p3row);
 
         int my_cnt = 0;
         for (int col = me; col < g.k; col += nthr) {

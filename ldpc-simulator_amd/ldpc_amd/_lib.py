@@ -37,7 +37,7 @@ EXPORTED = (
     "ldpc_phys_kernel_name", "ldpc_tile_lds_bytes", "ldpc_tile_kernel_name",
     "ldpc_decoder_bytes", "ldpc_decoder_create", "ldpc_decoder_destroy", "ldpc_decoder_capacity",
     "ldpc_decode_f64", "ldpc_generate_frames", "ldpc_mc_run",
-    "ldpc_profile_enable", "ldpc_profile_read", "ldpc_diag_tile_trace",
+    "ldpc_profile_enable", "ldpc_profile_read",
     "ldpc_phys_lds_bytes", "ldpc_phys_decode", "ldpc_phys_mc_run",
     "ldpc_comm_unique_id", "ldpc_comm_init", "ldpc_comm_allreduce", "ldpc_comm_barrier", "ldpc_comm_destroy",
     "ldpc_device_synchronize",
@@ -94,7 +94,6 @@ def _declare(lib):
         "ldpc_phys_mc_run": (ctypes.c_int, [c_vp, c_vp, c_u64, c_i32, P(c_dbl), c_i64, c_i64, c_i32, c_u32,
                                             P(c_i64), c_vp]),
         "ldpc_profile_read": (ctypes.c_int, [c_vp, P(c_dbl), P(c_i64)]),
-        "ldpc_diag_tile_trace": (ctypes.c_int, [c_vp, c_i64]),
         "ldpc_comm_unique_id": (ctypes.c_int, [c_vp]),
         "ldpc_comm_init": (ctypes.c_int, [c_vp, c_i32, c_i32, c_i32, P(c_vp)]),
         "ldpc_comm_allreduce": (ctypes.c_int, [c_vp, c_vp, c_i64, c_i32, c_i32, c_u32, c_vp]),

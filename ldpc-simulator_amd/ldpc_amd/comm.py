@@ -1,15 +1,19 @@
 """Multi-GPU counter exchange: RCCL behind the C ABI (no PyTorch).
 
-One process per GPU (the driver launches bench.py under torch.distributed.run,
-which only sets RANK / WORLD_SIZE / LOCAL_RANK / MASTER_PORT here).  Frames
+One process per GPU, started by torch.distributed.run or by bench.py's own
+launcher (bench.py --gpus N with no launcher around it); either sets RANK /
+WORLD_SIZE / LOCAL_RANK / MASTER_PORT, bench.py's launcher also LDPC_RDV_KEY.  Frames
 shard by global index (montecarlo.shard), so the one collective is the
 all-reduce of the int64 counter matrix -- the reference's parent-side sum of
 its workers' per-block results (python_ldpc_app/main.py:149-175).
 
 Rendezvous: rank 0 asks RCCL for a 128-byte unique id (ldpc_comm_unique_id)
-and publishes it in a file; the other ranks poll for it.  All ranks of one
-launch share the launcher's pid (os.getppid()) and MASTER_PORT, which name the
-file, so a stale file of an earlier launch is never read.  Single node only
+and publishes it in a file; the other ranks poll for it.  The file is named
+by a key every rank of ONE launch attempt shares and no other attempt does:
+LDPC_RDV_KEY when the launcher sets one (bench.py: a fresh uuid per launch),
+else the launcher's pid (os.getppid()) + MASTER_PORT + torchelastic's run id
+and restart count (an elastic restart keeps the agent pid and the port), so a
+stale file of an earlier launch or attempt is never read.  Single node only
 (--nnodes=1, as the driver runs it).
 """
 import ctypes
@@ -27,8 +31,17 @@ DT = {np.dtype(np.int64): 0, np.dtype(np.float64): 1}
 OPS = {"sum": 0, "max": 1}
 
 
+def rendezvous_key():
+    k = os.environ.get("LDPC_RDV_KEY")
+    if k:
+        return k
+    e = os.environ
+    return "_".join([str(os.getppid()), e.get("MASTER_PORT", "0"), e.get("TORCHELASTIC_RUN_ID", "none"),
+                     e.get("TORCHELASTIC_RESTART_COUNT", "0")])
+
+
 def rendezvous_path(key=None):
-    key = key or f"{os.getppid()}_{os.environ.get('MASTER_PORT', '0')}"
+    key = "".join(ch if ch.isalnum() or ch in "_-" else "-" for ch in (key or rendezvous_key()))
     return os.path.join(tempfile.gettempdir(), f"ldpc_rccl_{key}.id")
 
 
@@ -108,6 +121,11 @@ class Comm:
 
     def barrier(self):
         check("ldpc_comm_barrier", _lib.gpu().ldpc_comm_barrier(self._h))
+
+    def ranks_seen(self):
+        """How many ranks answer on this communicator: an RCCL sum of one per
+        rank (what ldpc_comm_barrier checks against world)."""
+        return int(self.allreduce(np.ones(1, np.int64))[0])
 
     def close(self):
         h = getattr(self, "_h", None)

@@ -13,8 +13,9 @@ Multi-GPU (one process per GPU): rank r decodes the global frame indices
 [r*B/W, (r+1)*B/W) of every SNR point -- the Philox stream is keyed by the
 global index, so the counters are identical for any W -- and the whole
 [points x 7] counter matrix is summed with ONE all-reduce: RCCL over xGMI
-through the C ABI (ldpc_amd.comm, no PyTorch); CPU tests inject a gloo
-reducer (torch_allreduce) to exercise the same sharding logic.
+through the C ABI (ldpc_amd.comm, no PyTorch); the CPU tests inject a gloo
+reducer of their own (tests/test_montecarlo.py) to exercise the same sharding
+logic.
 """
 import argparse
 import math
@@ -75,7 +76,7 @@ def run_sweep(decoder, snrs, blocks, max_iter, seed=20260213, nllr=False, speed=
     counter_fn  (sigmas, count, frame0) -> int64 [points, 7]; defaults to
                 decoder.mc_run (the GPU path).  Tests inject a CPU stand-in to
                 exercise the sharding/all-reduce logic without a GPU.
-    allreduce   callable(np.ndarray int64) -> summed array (torch.distributed wrapper)
+    allreduce   callable(np.ndarray int64) -> summed array (ldpc_amd.comm.Comm.allreduce)
     """
     sig = [sigma_for_snr(s, speed) for s in snrs]
     start, count = shard(int(blocks), rank, world)
@@ -88,20 +89,6 @@ def run_sweep(decoder, snrs, blocks, max_iter, seed=20260213, nllr=False, speed=
             raise ValueError("world > 1 needs an allreduce")
         local = np.asarray(allreduce(local), dtype=np.int64).reshape(len(snrs), NCOUNT)
     return local
-
-
-def torch_allreduce(device=None):
-    """ONE all-reduce of the counter matrix over the default process group."""
-    import torch
-    import torch.distributed as dist
-
-    def f(arr):
-        t = torch.from_numpy(np.ascontiguousarray(arr).reshape(-1).copy())
-        if device is not None:
-            t = t.to(device)
-        dist.all_reduce(t)
-        return t.cpu().numpy().reshape(arr.shape)
-    return f
 
 
 def simulate(matrix, snrs, blocks, max_iter, seed=20260213, nllr=False, chunk=65536, device=0,

@@ -61,6 +61,8 @@ def main():
     ap.add_argument("--threads", type=int, default=6)
     ap.add_argument("--points", default=DEFAULT_POINTS)
     ap.add_argument("--out", default=None)
+    ap.add_argument("--append", action="store_true",
+                    help="run points already in the file again and add the counts")
     a = ap.parse_args()
     CODE = a.code
     alist = os.path.join(REF_DB, "Wimax LDPC Codes", CODE + ".alist.txt")
@@ -74,11 +76,26 @@ def main():
     done = {p["snr_db"] for p in doc["points"]}
     with tempfile.TemporaryDirectory() as tmp:
         for snr, blocks in points:
-            if snr in done:
+            if snr in done and not a.append:
                 continue
             r = run_point(alist, snr, blocks, a.threads, tmp)
             r["threads"] = a.threads
             print(json.dumps(r), flush=True)
+            if snr in done:
+                # --append: another independent run of the reference at the same point
+                # (its RNG is time-seeded); the counts of the runs add up
+                p = next(q for q in doc["points"] if q["snr_db"] == snr)
+                runs = p.pop("runs", None) or [dict(p)]
+                runs.append(r)
+                p["blocks"] = sum(x["blocks"] for x in runs)
+                p["failed"] = sum(x["failed"] for x in runs)
+                p["err_bits"] = sum(x["err_bits"] for x in runs)
+                p["fer"] = p["failed"] / p["blocks"]
+                p["ber"] = sum(x["ber"] * x["blocks"] for x in runs) / p["blocks"]
+                p["wall_s"] = round(sum(x["wall_s"] for x in runs), 1)
+                p["runs"] = runs
+                json.dump(doc, open(a.out, "w"), indent=1)
+                continue
             doc["points"].append(r)
             doc["points"].sort(key=lambda p: p["snr_db"])
             json.dump(doc, open(a.out, "w"), indent=1)

@@ -275,7 +275,9 @@ def main():
         if want("w2304_T10"):
             run_set(pool, "w2304_T10", "wimax_2304_0.5", 10, [1.0, 2.0, 3.0], 4, True, 9000)
         if want("w2304_T50"):
-            run_set(pool, "w2304_T50", "wimax_2304_0.5", 50, [1.0, 3.0], 2, False, 9500)
+            # round 3: 16 frames per point (the first 2 of each keep round 2's seeds);
+            # 1 dB is config 3's timed point -- 50 saturating iterations per frame
+            run_set(pool, "w2304_T50", "wimax_2304_0.5", 50, [1.0, 3.0], 16, False, 9500)
         if want("w2304A_T3_4dB"):  # the r3/4A FER-1.0 cliff, in the reference itself
             run_set(pool, "w2304A_T3_4dB", "wimax_2304_0.75A", 3, [4.0], 4, False, 10000)
         if want("w2304B_T2"):

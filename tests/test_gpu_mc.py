@@ -24,7 +24,7 @@ def _decoder(code, frames):
     return Decoder(Graph.cached(hstd_for(code)), frames)
 
 
-@pytest.mark.parametrize("code", ["BCH_7_4_1_strip", "wimax_576_0.5", "wimax_2304_0.75A"])
+@pytest.mark.parametrize("code", ["BCH_7_4_1_strip", "wimax_576_0.5", "wimax_2304_0.5", "wimax_2304_0.75A"])
 def test_generator_matches_cpu_restatement(gpu_available, code):
     H = hstd_for(code)
     dec = _decoder(code, 96)

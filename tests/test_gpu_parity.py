@@ -62,6 +62,10 @@ def _random_llr(H, B, snr_db, seed):
     ("wimax_576_0.5", 200, 8, 1.5),
     ("wimax_576_0.5", 130, 20, 2.5),
     ("wimax_2304_0.75A", 64, 3, 3.0),
+    # the north-star code at config 3's point: 50 saturating iterations at 1 dB
+    # (where the GPU's atanh and the reference's SVML arctanh could part at the ulp)
+    ("wimax_2304_0.5", 64, 50, 1.0),
+    ("wimax_2304_0.5", 70, 50, 2.0),   # ragged: one full and one partial 64-frame tile
 ])
 def test_gpu_matches_oracle_random(gpu_available, code, B, T, snr):
     H = hstd_for(code)

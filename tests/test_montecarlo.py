@@ -103,13 +103,23 @@ def _free_port():
         return s.getsockname()[1]
 
 
+def gloo_allreduce(arr):
+    """ONE all-reduce of the counter matrix over the default (gloo) process
+    group: the CPU stand-in for ldpc_amd.comm.Comm.allreduce (RCCL)."""
+    import torch
+    import torch.distributed as dist
+    t = torch.from_numpy(np.ascontiguousarray(arr).reshape(-1).copy())
+    dist.all_reduce(t)
+    return t.numpy().reshape(arr.shape)
+
+
 def _rank_main(rank, world, port, outdir):
     import torch.distributed as dist
     dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
     try:
         f = oracle_counter_fn("wimax_576_0.5", 4)
         ctr = mc.run_sweep(None, [0.0, 1.5, 3.0], 37, 4, rank=rank, world=world,
-                           allreduce=mc.torch_allreduce(None), counter_fn=f)
+                           allreduce=gloo_allreduce, counter_fn=f)
         np.save(os.path.join(outdir, f"rank{rank}.npy"), ctr)
     finally:
         dist.destroy_process_group()
