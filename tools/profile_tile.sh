@@ -8,12 +8,12 @@
 # usage: tools/profile_tile.sh TAG ; outputs under gpurun_out/TAG
 set -e
 TAG=${1:-prof_tile}
-ARGS="--steps 2 --warmup 1 --cpu-seconds 0 --extra-snr="
+ARGS="--steps 2 --warmup 1 --cpu-seconds 0 --extra-snr= --phys-steps 0"
 export TMPDIR=/tmp
 OUT=gpurun_out/$TAG
 mkdir -p $OUT
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o run -- python3 bench.py $ARGS > $OUT/bench_trace.log 2>&1
 timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/pmc_fetch -o run -- python3 bench.py $ARGS > $OUT/bench_fetch.log 2>&1
-timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/pmc_fetch_split -o run -- python3 bench.py --split --steps 1 --warmup 0 --iters 4 --cpu-seconds 0 --extra-snr= > $OUT/bench_fetch_split.log 2>&1
+timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/pmc_fetch_split -o run -- python3 bench.py --split --steps 1 --warmup 0 --iters 4 --cpu-seconds 0 --extra-snr= --phys-steps 0 > $OUT/bench_fetch_split.log 2>&1
 timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/pmc_write -o run -- python3 bench.py $ARGS > $OUT/bench_write.log 2>&1
 echo done
