@@ -93,11 +93,14 @@ namespace {
 // w's.  Chunking as sub_chunk: C = ceil(deg / 16) edges per wavefront.  An
 // empty chunk waits for nothing (lo > hi); after an empty row, every
 // wavefront waits for all 16 (whose in-order P3s then cover every row before).
-std::vector<int> sub_p3_deps(int m, const int *row_ptr, const int *col_idx) {
+// drop_last: chunk all but each row's last edge (tile8.hip: the identity
+// column k + r of an [A | I_m] row is wavefront 0's, outside the chunks).
+std::vector<int> sub_p3_deps(int m, const int *row_ptr, const int *col_idx, bool drop_last = false) {
     constexpr int W = ldpc::kSubWaves;
     std::vector<int> dep((size_t)m * W, 1);  // lo 1 > hi 0: no wait
     auto spans = [&](int r, long long lo[W], long long hi[W], bool ne[W]) {
-        const int beg = row_ptr[r], deg = row_ptr[r + 1] - beg, C = (deg + W - 1) / W;
+        const int beg = row_ptr[r];
+        const int deg = std::max(0, row_ptr[r + 1] - beg - (drop_last ? 1 : 0)), C = (deg + W - 1) / W;
         long long prev = -1;
         int last = -1;
         for (int w = 0; w < W; ++w) {
@@ -387,7 +390,8 @@ int ldpc_graph_create(int32_t m, int32_t n, const int32_t *row_ptr, const int32_
     DeviceGuard dg(device);
     if (device < 0) (void)hipGetDevice(&g->device);
     const std::vector<int> p3dep = sub_p3_deps(m, row_ptr, col_idx);
-    const size_t nints = (size_t)(m + 1) + nnz + (size_t)(n + 1) + 2 * (size_t)nnz + p3dep.size();
+    const std::vector<int> p3dep8 = sub_p3_deps(m, row_ptr, col_idx, true);
+    const size_t nints = (size_t)(m + 1) + nnz + (size_t)(n + 1) + 2 * (size_t)nnz + p3dep.size() + p3dep8.size();
     if (int rc = dev_alloc(&g->d_ints, nints)) {
         delete g;
         return rc;
@@ -402,6 +406,7 @@ int ldpc_graph_create(int32_t m, int32_t n, const int32_t *row_ptr, const int32_
     G.max_col_deg = max_col;
     G.std_form = std_form;
     G.ira = ira;
+    G.ef = kTile;
     G.row_ptr = p;
     p += m + 1;
     G.col_idx = p;
@@ -413,6 +418,8 @@ int ldpc_graph_create(int32_t m, int32_t n, const int32_t *row_ptr, const int32_
     G.csc_row = p;
     p += nnz;
     G.p3dep = p;
+    p += p3dep.size();
+    G.p3dep8 = p;
     hipError_t e = hipSuccess;
     if (e == hipSuccess) e = hipMemcpy((void *)G.row_ptr, row_ptr, sizeof(int) * (m + 1), hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMemcpy((void *)G.col_idx, col_idx, sizeof(int) * nnz, hipMemcpyHostToDevice);
@@ -421,6 +428,8 @@ int ldpc_graph_create(int32_t m, int32_t n, const int32_t *row_ptr, const int32_
     if (e == hipSuccess) e = hipMemcpy((void *)G.csc_row, csc_row.data(), sizeof(int) * nnz, hipMemcpyHostToDevice);
     if (e == hipSuccess && m > 0)
         e = hipMemcpy((void *)G.p3dep, p3dep.data(), sizeof(int) * p3dep.size(), hipMemcpyHostToDevice);
+    if (e == hipSuccess && m > 0)
+        e = hipMemcpy((void *)G.p3dep8, p3dep8.data(), sizeof(int) * p3dep8.size(), hipMemcpyHostToDevice);
     if (e == hipSuccess && std_form && k > 0) {  // encoder table: A bit-packed per row
         const size_t kw = (size_t)(k + 31) / 32;
         std::vector<uint32_t> ap((size_t)m * kw, 0u);
@@ -432,6 +441,8 @@ int ldpc_graph_create(int32_t m, int32_t n, const int32_t *row_ptr, const int32_
             e = hipMemcpy(g->d_apack, ap.data(), sizeof(uint32_t) * ap.size(), hipMemcpyHostToDevice);
         G.a_packed = g->d_apack;
     }
+    // the WiMAX 2304 codes run the 8-frame sub-tile decoder: E in 8-frame blocks
+    if (e == hipSuccess && !ldpc::tile64_lds_bytes(G) && ldpc::tile8_applies(G)) G.ef = 8;
     if (e != hipSuccess) {
         (void)hipFree(g->d_ints);
         (void)hipFree(g->d_apack);

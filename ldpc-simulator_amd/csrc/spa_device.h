@@ -5,7 +5,8 @@
 // [tile][item][64 lanes], so a wavefront touching item i of its tile reads
 // 64 consecutive doubles (512 contiguous bytes): fully coalesced, with no
 // index math per lane.
-//   E   [tile][nnz][64]  fp64 check->variable messages (CSR edge order of H_std)
+//   E   [tile][nnz][64]  fp64 check->variable messages (CSR edge order of H_std);
+//                        for tile8.hip's graphs [tile][8][nnz][8] (e_base below)
 //   T   [slot][max_row_deg][64] fp64 scratch of cn_rare_kernel (slot = its
 //                        global wavefront id; nslots = 4 x its grid)
 //   L   [tile][n][64]    fp64 a-posteriori LLRs
@@ -40,7 +41,17 @@ struct DevGraph {
     const int *csc_row;      // [nnz] row of that edge
     const uint32_t *a_packed;  // [m][kw] bit j of row r = A[r][j] (encoder; std_form only)
     const int *p3dep;          // [m][16] sub-tile S order: lo | hi << 8 (tile_sub.hip sub_p3)
+    const int *p3dep8;         // [m][16] the same over each row's A edges (tile8.hip: identity excluded)
+    int ef;                    // frames per E block (64, or 8 for tile8.hip's graphs): e_base
 };
+
+// E layout inside a tile: the 64 frames in blocks of g.ef, each block
+// [nnz][ef], so a workgroup that decodes ef frames reads whole cache lines
+// (ef = 64: [tile][nnz][64]; ef = 8: [tile][8][nnz][8], the 8-frame sub-tile
+// decoder of tile8.hip).  Element (tile, e, lane) = E[e_base(tile, lane) + e * ef].
+__host__ __device__ inline size_t e_base(const DevGraph &g, int tile, int lane) {
+    return (size_t)tile * g.nnz * kTile + (size_t)(lane / g.ef) * g.nnz * g.ef + (size_t)(lane % g.ef);
+}
 
 struct DevState {
     double *E, *T, *L, *ch;
@@ -97,6 +108,12 @@ bool use_tile_stream(const DevGraph &g);
 hipError_t launch_tile_stream(const DevGraph &g, const DevState &st, int max_iter, bool nllr, uint64_t seed,
                               int snr_point, double sigma, int64_t frame0, int64_t total, unsigned long long *next,
                               unsigned long long *ctr, int64_t handoff, hipStream_t s);
+// 8-frame sub-tile decoder (tile8.hip): the WiMAX 2304 codes; its graphs keep
+// E in 8-frame blocks (DevGraph::ef = 8, chosen at graph creation)
+bool tile8_applies(const DevGraph &g);
+size_t tile8_lds_bytes(const DevGraph &g);
+hipError_t launch_tile8(const DevGraph &g, const DevState &st, int max_iter, bool nllr, hipStream_t s);
+size_t tile64_lds_bytes(const DevGraph &g);  // tile_kernel (64 frames per workgroup), 0 if it does not apply
 int sub_frames(const DevGraph &g);
 size_t sub_lds_bytes(const DevGraph &g);
 hipError_t launch_tile_sub(const DevGraph &g, const DevState &st, int max_iter, bool nllr, hipStream_t s);

@@ -87,12 +87,12 @@ template <bool kFirst, bool kStream>
 struct EdgeStream {
     const int *__restrict__ col;
     const double *Lt, *Et;
-    int end;
+    int end, es;  // es: E stride between edges (DevGraph::ef)
     bool fresh;
     double lv[kPf], eo[kPf];
     __device__ __forceinline__ EdgeStream(const int *__restrict__ col_, const double *L_, const double *E_, int beg,
-                                          int end_, bool fresh_)
-        : col(col_), Lt(L_), Et(E_), end(end_), fresh(fresh_) {
+                                          int end_, bool fresh_, int es_)
+        : col(col_), Lt(L_), Et(E_), end(end_), es(es_), fresh(fresh_) {
 #pragma unroll
         for (int k = 0; k < kPf; ++k) fetch(k, beg + k);
     }
@@ -101,7 +101,7 @@ struct EdgeStream {
         // keeps the ring in place and waits only for the slot it consumes
         const int i = e < end ? e : end - 1;
         lv[k] = Lt[col[i] * kTile];  // col[] is read-only + noalias -> scalar load
-        eo[k] = kFirst ? 0.0 : ld_e(&Et[i * kTile]);
+        eo[k] = kFirst ? 0.0 : ld_e(&Et[(size_t)i * es]);
     }
     __device__ __forceinline__ double take(int k, int e) {
         const double M = kFirst ? lv[k] : lv[k] - ((kStream && fresh) ? 0.0 : eo[k]);
@@ -135,7 +135,7 @@ __global__ __launch_bounds__(256, LDPC_CN_WAVES) void cn_kernel(DevGraph g, DevS
     const int f = tile * kTile + lane;
     const bool live = st.done[f] == 0;
     const bool fresh = kStream && st.fresh[f] != 0;
-    double *Et = st.E + (size_t)tile * g.nnz * kTile + lane;
+    double *Et = st.E + e_base(g, tile, lane);
     const double *Lt = (kFirst ? st.ch : st.L) + (size_t)tile * g.n * kTile + lane;
 
     // Both passes stream (L[col], E_old) through a register ring of kPf
@@ -144,7 +144,7 @@ __global__ __launch_bounds__(256, LDPC_CN_WAVES) void cn_kernel(DevGraph g, DevS
     double P = 1.0;
     bool tiny = false;
     {
-        EdgeStream<kFirst, kStream> es(col_idx, Lt, Et, beg, end, fresh);
+        EdgeStream<kFirst, kStream> es(col_idx, Lt, Et, beg, end, fresh, g.ef);
         for (int e = beg; e < end; e += kPf) {
 #pragma unroll
             for (int k = 0; k < kPf; ++k) {
@@ -161,7 +161,7 @@ __global__ __launch_bounds__(256, LDPC_CN_WAVES) void cn_kernel(DevGraph g, DevS
         // pass 2: recompute t from the same E_old / L bits (identical result),
         // E_new = 2 atanh(clip(P/t)) written over E_old.  24 B of HBM per edge
         // instead of parking t (32 B).
-        EdgeStream<kFirst, kStream> es(col_idx, Lt, Et, beg, end, fresh);
+        EdgeStream<kFirst, kStream> es(col_idx, Lt, Et, beg, end, fresh, g.ef);
         const bool nr = div_nr_ok(P);  // wave-uniform (cn_common.h)
         for (int e = beg; e < end; e += kPf) {
 #pragma unroll
@@ -170,7 +170,7 @@ __global__ __launch_bounds__(256, LDPC_CN_WAVES) void cn_kernel(DevGraph g, DevS
                 if (e + k < end) {  // wave-uniform
                     const double t = cn_tanh(M, ttab);
                     const double En = 2.0 * atanh_f(clip_cl(nr ? div_nr(P, t) : P / t), ltab, ac);
-                    if (live) st_e(&Et[(e + k) * kTile], En);
+                    if (live) st_e(&Et[(size_t)(e + k) * g.ef], En);
                 }
             }
         }
@@ -234,7 +234,7 @@ __global__ __launch_bounds__(64 * W, WPS) void cn_row_kernel(DevGraph g, DevStat
     const int f = tile * kTile + lane;
     const bool live = st.done[f] == 0;
     const bool fresh = kStream && st.fresh[f] != 0;
-    double *Et = st.E + (size_t)tile * g.nnz * kTile + lane;
+    double *Et = st.E + e_base(g, tile, lane);
     const double *Lt = (kFirst ? st.ch : st.L) + (size_t)tile * g.n * kTile + lane;
     const int C = (deg + W - 1) / W;
     const int c0 = beg + wave * C;
@@ -251,7 +251,7 @@ __global__ __launch_bounds__(64 * W, WPS) void cn_row_kernel(DevGraph g, DevStat
             for (int i = h * H; i < (h + 1) * H; ++i) {
                 const int e = c0 + min(i, cnt - 1);
                 t[i] = Lt[col_idx[e] * kTile];
-                eo[i - h * H] = kFirst ? 0.0 : ld_e(&Et[e * kTile]);
+                eo[i - h * H] = kFirst ? 0.0 : ld_e(&Et[(size_t)e * g.ef]);
             }
 #pragma unroll
             for (int i = h * H; i < (h + 1) * H; ++i) {
@@ -286,7 +286,7 @@ __global__ __launch_bounds__(64 * W, WPS) void cn_row_kernel(DevGraph g, DevStat
         for (int i = 0; i < K; ++i) {
             if (i < cnt) {
                 const double En = 2.0 * atanh_f(clip_cl(div_nr(P, t[i])), ltab, ac);
-                if (live) st_e(&Et[(c0 + i) * kTile], En);
+                if (live) st_e(&Et[(size_t)(c0 + i) * g.ef], En);
             }
         }
         return;
@@ -295,7 +295,7 @@ __global__ __launch_bounds__(64 * W, WPS) void cn_row_kernel(DevGraph g, DevStat
     for (int i = 0; i < K; ++i) {
         if (i < cnt) {
             const double En = 2.0 * atanh_f(clip_cl(P / t[i]), ltab, ac);
-            if (live) st_e(&Et[(c0 + i) * kTile], En);
+            if (live) st_e(&Et[(size_t)(c0 + i) * g.ef], En);
         }
     }
 }
@@ -323,12 +323,12 @@ __global__ __launch_bounds__(256) void cn_rare_kernel(DevGraph g, DevState st, i
         const int f = tile * kTile + lane;
         const bool live = st.done[f] == 0;
         const bool fresh = kStream && st.fresh[f] != 0;
-        double *Et = st.E + (size_t)tile * g.nnz * kTile + lane;
+        double *Et = st.E + e_base(g, tile, lane);
         const double *Lt = (kFirst ? st.ch : st.L) + (size_t)tile * g.n * kTile + lane;
         double P = 1.0;
         for (int e = beg; e < end; ++e) {
             double M = Lt[g.col_idx[e] * kTile];
-            if (!kFirst) M = M - (fresh ? 0.0 : Et[e * kTile]);
+            if (!kFirst) M = M - (fresh ? 0.0 : Et[(size_t)e * g.ef]);
             const double t = cn_tanh(M, ttab);
             P = (e == beg) ? t : P * t;
             Tt[(e - beg) * kTile] = t;
@@ -349,7 +349,7 @@ __global__ __launch_bounds__(256) void cn_rare_kernel(DevGraph g, DevState st, i
                 }
             }
             const double En = 2.0 * atanh_f(clip_cl(q), ltab, ac);
-            if (live) Et[e * kTile] = En;
+            if (live) Et[(size_t)e * g.ef] = En;
         }
     }
 }
@@ -391,7 +391,7 @@ __global__ __launch_bounds__(1024) void vn_kernel(DevGraph g, DevState st, int i
     const int kw = (g.k + 31) >> 5;
     const uint32_t *Ut = st.ubits + (size_t)tile * kw * kTile + lane;
     int my_err = 0;
-    const double *Et = st.E + (size_t)tile * g.nnz * kTile + lane;
+    const double *Et = st.E + e_base(g, tile, lane);
     double *Lt = st.L + (size_t)tile * g.n * kTile + lane;
     const double *Ct = st.ch + (size_t)tile * g.n * kTile + lane;
 
@@ -403,12 +403,12 @@ __global__ __launch_bounds__(1024) void vn_kernel(DevGraph g, DevState st, int i
             // ring of kPv loads in flight (indices clamped into the column)
             double ring[kPv];
 #pragma unroll
-            for (int k = 0; k < kPv; ++k) ring[k] = ld_e(&Et[csc_edge[min(p0 + k, p1 - 1)] * kTile]);
+            for (int k = 0; k < kPv; ++k) ring[k] = ld_e(&Et[(size_t)csc_edge[min(p0 + k, p1 - 1)] * g.ef]);
             for (int p = p0; p < p1; p += kPv) {
 #pragma unroll
                 for (int k = 0; k < kPv; ++k) {
                     const double v = ring[k];
-                    ring[k] = ld_e(&Et[csc_edge[min(p + k + kPv, p1 - 1)] * kTile]);
+                    ring[k] = ld_e(&Et[(size_t)csc_edge[min(p + k + kPv, p1 - 1)] * g.ef]);
                     if (p + k < p1) s = s + v;
                 }
             }
@@ -513,17 +513,17 @@ __global__ __launch_bounds__(256) void vn_cols_kernel(DevGraph g, DevState st, i
     const int lane = threadIdx.x & 63;
     const int f = tile * kTile + lane;
     const bool live = st.done[f] == 0;
-    const double *Et = st.E + (size_t)tile * g.nnz * kTile + lane;
+    const double *Et = st.E + e_base(g, tile, lane);
     const int p0 = g.csc_ptr[j], p1 = g.csc_ptr[j + 1];
     double s = 0.0;  // rows ascending, starting at 0.0
     double ring[kTv];
 #pragma unroll
-    for (int q = 0; q < kTv; ++q) ring[q] = Et[(size_t)g.csc_edge[min(p0 + q, p1 - 1)] * kTile];
+    for (int q = 0; q < kTv; ++q) ring[q] = Et[(size_t)g.csc_edge[min(p0 + q, p1 - 1)] * g.ef];
     for (int p = p0; p < p1; p += kTv) {
 #pragma unroll
         for (int q = 0; q < kTv; ++q) {
             const double v = ring[q];
-            ring[q] = Et[(size_t)g.csc_edge[min(p + q + kTv, p1 - 1)] * kTile];
+            ring[q] = Et[(size_t)g.csc_edge[min(p + q + kTv, p1 - 1)] * g.ef];
             if (p + q < p1) s = s + v;
         }
     }
@@ -678,7 +678,7 @@ __global__ void export_msgs_kernel(DevGraph g, DevState st, double *out) {
     if (i >= total) return;
     const int f = (int)(i / g.nnz);
     const int e = (int)(i % g.nnz);
-    out[i] = st.E[((size_t)(f >> 6) * g.nnz + e) * kTile + (f & 63)];
+    out[i] = st.E[e_base(g, f >> 6, f & 63) + (size_t)e * g.ef];
 }
 
 // Streaming refill (Monte-Carlo path): every lane flagged by vn_kernel (or, at
@@ -945,7 +945,7 @@ __global__ void compact_move_kernel(DevGraph g, DevState st, int cap, const int 
         const int src = pairs[1 + p], dst = pairs[1 + cap + p];
         const size_t st_ = src >> 6, sl = src & 63, dt = dst >> 6, dl = dst & 63;
         if (it < g.nnz) {
-            st.E[(dt * g.nnz + it) * kTile + dl] = st.E[(st_ * g.nnz + it) * kTile + sl];
+            st.E[e_base(g, (int)dt, (int)dl) + (size_t)it * g.ef] = st.E[e_base(g, (int)st_, (int)sl) + (size_t)it * g.ef];
             continue;
         }
         it -= g.nnz;

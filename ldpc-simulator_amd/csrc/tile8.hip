@@ -1,0 +1,810 @@
+// tile8.hip -- the tile-resident parity decoder of the WiMAX 2304 codes,
+// 8 frames per workgroup (gfx950).
+//
+// Reference: python_ldpc_app/spa_decoder.py:63-280 (SPA_Decoder.decode): per
+// check row r (:112-168) t_e = tanh(M_e/2) clipped, P = t_0 * t_1 * ... left to
+// right in ascending column order, E_e = 2 atanh(clip(P / t_e)); per column
+// (:173-185) S_j = ((0 + E_r0j) + E_r1j) + ... rows ascending, L_j = ch_j + S_j;
+// hard decision, syndrome on z^1 and early termination (:188-253); M = L - E
+// (:260-268).  Every fp64 operation is the reference's, in its order.
+//
+// Why 8 frames: the column sums S of a workgroup's frames must sit in LDS
+// (k x F x 8 B) and the posteriors L of the A columns are gathered by every
+// edge.  With F = 8, wimax_2304_0.5 keeps BOTH in LDS (S and L_A: 2 x 72 KB),
+// so the only global traffic left in the row loop is the message stream E
+// (read once, written once per iteration: the algorithmic 16 B per edge) and
+// one identity-column posterior per row; the r3/4 codes (k = 1728) keep S in
+// LDS (108 KB) and gather L from L2 (108 KB per workgroup: 3.5 MB per XCD,
+// L2-resident).  Registers hold 3 rows of t (pipeline depth D = 3) and the
+// next row's E_old, prefetched one row ahead.  E is laid out in 8-frame blocks
+// (DevGraph::ef = 8, spa_device.h e_base) so a lane group's 8 frames of one
+// edge are 64 contiguous bytes and two consecutive edges share a cache line.
+//
+// Mapping: lane = j * 8 + f (lane group j = 0..7, frame f).  A row of an
+// [A | I_m] graph is its A edges and, last, the identity column k + r.  The A
+// edges are split into 16 contiguous wavefront chunks (wavefront w: positions
+// [w*C, w*C + C), C = ceil((deg-1)/16): the host-built P3 order table p3dep8
+// assumes this chunking) and a chunk into 8 contiguous lane-group pieces of
+// CS = ceil(C/8) edges (slot i of group j = position j*CS + i).  The product
+// of the A edges crosses lane groups inside a wavefront by DPP row shifts and
+// permlane swaps (VALU only, branch-free) and wavefronts through an LDS slot +
+// epoch flag; the identity edge belongs to one wavefront (t_id in P1, E_id and
+// L_id in P3: wavefront 0 at D = 3, where it otherwise waits longest for the
+// chain; the last one at D = 2),
+// and every P3 takes P = P_A * t_id: the reference's left-to-right order.
+//
+// Per wavefront, body(r) = prefetch(r+1), hop(r), P3(r-D+1), P1(r+1):
+//   hop(r)     this wavefront's piece of row r's left-to-right product;
+//   P3(r')     E_new = 2 atanh(clip(P/t)), stored; S_col += E_new, after the
+//              wavefronts whose column spans overlap finished P3(r'-1);
+//   P1(r+1)    M = L[col] - E_old, t = tanh(M/2) (clipped).
+// D = 3 gives a row's chain two bodies to cross all 16 wavefronts before its
+// P3 needs the final product.
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstdlib>
+
+#include "cn_common.h"
+#include "frame_source.h"
+#include "spa_device.h"
+#include "spa_math.h"
+#include "tile_common.h"
+
+namespace ldpc {
+namespace {
+
+constexpr int kW8 = kSubWaves;  // 16 wavefronts per workgroup (p3dep chunking)
+constexpr int kF8 = 8;          // frames per workgroup
+constexpr int kQ8 = 8;          // lane groups per wavefront
+constexpr int kSR8 = 8;         // chain slots (>= 2 D: a slot is reused only after every P3 of its row)
+constexpr size_t kLds8Max = 163840;
+// Scheduling fences between the slots of P1 (tanh) and P3 (atanh): without
+// them the compiler interleaves all K slots' math for ILP and spills; the
+// four wavefronts of a SIMD supply the overlap instead.
+#ifndef LDPC_T8_SLOT_FENCE
+#define LDPC_T8_SLOT_FENCE 0
+#endif
+__device__ __forceinline__ void t8_slot_fence() {
+#if LDPC_T8_SLOT_FENCE
+    __builtin_amdgcn_sched_barrier(0);
+#endif
+}
+
+// -DLDPC_T8_TIMERS: diagnostic build (never the product) -- s_memtime phase
+// timers per wavefront, printed for two workgroups at the end of the launch.
+#ifdef LDPC_T8_TIMERS
+#define T8_NT 9  // hop wait, hop, P3 chain wait, P3 math+stores, P3 order wait, P3 S adds, P1, prefetch, rows
+#define T8_STAMP(v) const uint64_t v = __builtin_amdgcn_s_memtime()
+#define T8_ADD(c, i, a, b) ((c).tm[i] += (b) - (a))
+#else
+#define T8_STAMP(v)
+#define T8_ADD(c, i, a, b)
+#endif
+
+// logical wavefront (chunk position) of hardware wavefront hw: the four
+// wavefronts of one SIMD take four consecutive chunk positions (as tile_sub.hip)
+__device__ __forceinline__ int t8_wave(int hw) { return (hw & 3) * 4 + (hw >> 2); }
+
+// Global accesses go through buffer resources built from wave-uniform bases
+// (this workgroup's E block, its tile's L / ch): a 32-bit per-lane voffset,
+// the base in SGPRs -- the compiler cannot hoist 64-bit per-lane pointers
+// out of the row loop (they spilled, and a scratch reload's vmcnt(0) drained
+// the prefetched E_old).  NT = non-temporal (the message stream).
+typedef unsigned int t8u2 __attribute__((ext_vector_type(2)));
+constexpr int kNT = 2;
+// a voffset past every buffer's num_records: the hardware drops such a store
+// (and a load returns 0) -- masked stores without a branch
+constexpr uint32_t kOOB = 0xfffffff0u;
+template <int AUX = 0>
+__device__ __forceinline__ double t8_ld(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+    return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, AUX));
+}
+template <int AUX = 0>
+__device__ __forceinline__ void t8_st(__amdgpu_buffer_rsrc_t r, uint32_t off, double v) {
+    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(t8u2, v), r, off, 0, AUX);
+}
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t t8_rsrc(const void *base, size_t bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(base), (short)0, (int)min(bytes, (size_t)0x7fffffff),
+                                            0x00020000);
+}
+
+struct T8Layout {
+    size_t S, LA, math, slot, zb, ib, lane_i, flags, dummy, cidx, total;
+};
+// R: rows of staged column indices per wavefront (D + 1: P3's row r-D+2 ..
+// the staged row r+2 of body(r+1))
+__host__ __device__ inline T8Layout t8_layout(int k, int m, int K, bool la, int R) {
+    T8Layout t;
+    size_t o = 0;
+    t.S = o;  // [k][8] column sums
+    o = al16(o + (size_t)k * kF8 * sizeof(double));
+    t.LA = o;  // [k][8] posteriors of the A columns (previous iteration)
+    if (la) o = al16(o + (size_t)k * kF8 * sizeof(double));
+    t.math = o;
+    o = al16(o + sizeof(MathLds));
+    t.slot = o;  // [kSR8][8] chain slots, then [kSR8][8] t of the identity edge
+    o = al16(o + 2 * kSR8 * (size_t)kF8 * sizeof(double));
+    t.zb = o;  // [kw][8] z^1 bits of the A columns
+    o = al16(o + (size_t)((k + 31) / 32) * kF8 * sizeof(uint32_t));
+    t.ib = o;  // [mw][8] z^1 bits of the identity columns
+    o = al16(o + (size_t)((m + 31) / 32) * kF8 * sizeof(uint32_t));
+    t.lane_i = o;  // bad[8], nllr count[8], live[8], it[8], fresh[8]
+    o = al16(o + 5 * (size_t)kF8 * sizeof(int));
+    t.flags = o;  // chain flag[kSR8], tiny[kSR8], tiny sequence, running, p3row[16]
+    o = al16(o + (2 * kSR8 + 2 + kW8) * sizeof(int));
+    t.dummy = o;  // [8] target of masked-off S updates
+    o = al16(o + (size_t)kF8 * sizeof(double));
+    t.cidx = o;  // [R][16][8*K] uint16 column indices, one wavefront chunk per row
+    o = al16(o + (size_t)R * kW8 * kQ8 * K * sizeof(uint16_t));
+    t.total = o;
+    return t;
+}
+
+// deg: the whole row; the chunks cover its A edges (all but the last, the
+// identity column k + r at edge eid = beg + deg - 1).
+struct T8Chunk {
+    int deg, beg, c0, cnt, CS;
+};
+__device__ __forceinline__ T8Chunk t8_chunk(const int *__restrict__ row_ptr, int r, int wave) {
+    T8Chunk c;
+    c.beg = row_ptr[r];
+    c.deg = row_ptr[r + 1] - c.beg;
+    const int da = max(c.deg - 1, 0);
+    const int C = (da + kW8 - 1) / kW8;
+    c.c0 = c.beg + wave * C;
+    c.cnt = max(0, min(da - wave * C, C));
+    c.CS = (C + kQ8 - 1) / kQ8;
+    return c;
+}
+
+template <int K>
+struct T8Ctx {
+    const int *__restrict__ col_idx;
+    const int *__restrict__ row_ptr;
+    const int *p3dep;
+    // buffer resources (uniform) + per-lane byte offsets eo8 (E block: f * 8)
+    // and lo8 (L / ch: (sub*8 + f) * 8)
+    __amdgpu_buffer_rsrc_t rE;  // this workgroup's E block: edge e, frame f at e*64 + f*8
+    __amdgpu_buffer_rsrc_t rL, rC;  // the tile's L / ch: column c at c*512 + lo8
+    uint32_t eo8, lo8;
+    double *Tb;      // rare-row scratch of this workgroup, position p at [p * 8]
+    double *S;       // LDS, column c at [c * 8] (this lane's frame added)
+    double *LA;      // LDS, same indexing (null: L gathered from global)
+    double *dummy;   // LDS, this lane's frame
+    double *slot;    // LDS, chain slot s at [s * 8]; t of row s's identity edge at [(kSR8 + s) * 8]
+    uint32_t *ib;    // LDS, word w at [w * 8]
+    uint16_t *cidx;  // LDS, this wavefront's ring: row slot q, position p at [q * 16 * 8K + p]
+    int *flag, *tinyf, *tseq, *p3row;
+    LdsTanh ttab;
+    LdsLog ltab;
+    AtanhCoef ac;
+    int m, k, wave, j, f;
+    int ep0;
+    bool first, live, fresh;
+    int ntiny;
+    int R;       // ring rows
+    int idwave;  // the wavefront that owns the identity edge
+#ifdef LDPC_T8_TIMERS
+    uint64_t tm[T8_NT];
+#endif
+};
+
+// This lane's edge count in chunk rc.
+template <int K>
+__device__ __forceinline__ int t8_nj(const T8Ctx<K> &c, const T8Chunk &rc) {
+    return max(0, min(rc.cnt - c.j * rc.CS, rc.CS));
+}
+// Byte offset (from c.Eu) of this lane's slot 0 in chunk rc; slot i at + i * 64.
+// Slots past the lane's piece read other edges (or the allocation's
+// kEPadEdges slack) and are discarded.
+template <int K>
+__device__ __forceinline__ uint32_t t8_eoff(const T8Ctx<K> &c, const T8Chunk &rc) {
+    return ((uint32_t)(rc.c0 + c.j * rc.CS) << 6) + c.eo8;
+}
+template <int K>
+__device__ __forceinline__ uint32_t t8_es(const T8Ctx<K> &c, uint32_t off, int i) {
+    return off + (uint32_t)i * (kF8 * sizeof(double));
+}
+
+// Staging of row q's column indices into the ring: issue (one index per lane,
+// lanes < the chunk size), commit once the wavefront has waited anyway.
+template <int K>
+__device__ __forceinline__ int t8_stage_issue(const T8Ctx<K> &c, int q) {
+    if (q >= c.m) return 0;
+    const T8Chunk rc = t8_chunk(c.row_ptr, q, c.wave);
+    const int L = threadIdx.x & 63;
+    return rc.cnt > 0 ? c.col_idx[rc.c0 + min(L, rc.cnt - 1)] : 0;
+}
+template <int K>
+__device__ __forceinline__ void t8_stage_commit(const T8Ctx<K> &c, int q, int v) {
+    if (q >= c.m) return;
+    constexpr int W = kQ8 * K;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    if ((int)(threadIdx.x & 63) < W) c.cidx[(q % c.R) * kW8 * W + (threadIdx.x & 63)] = (uint16_t)v;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+template <int K>
+__device__ __forceinline__ const uint16_t *t8_lcols(const T8Ctx<K> &c, int r, const T8Chunk &rc) {
+    return c.cidx + (r % c.R) * kW8 * kQ8 * K + c.j * rc.CS;
+}
+
+// Next row's loads that do not depend on the staged indices: E_old of this
+// lane's K slots and the identity column's posterior (L[k+r], or ch[k+r] on
+// iteration 0 / a fresh frame's first pass).
+template <int K>
+struct T8Pre {
+    double eo[K];
+    double lid, eid;  // wavefront 0: the identity column's posterior and E_old
+};
+template <int K>
+__device__ __forceinline__ void t8_prefetch(const T8Ctx<K> &c, int r, T8Pre<K> &p) {
+    const T8Chunk rc = t8_chunk(c.row_ptr, r, c.wave);
+    if (rc.cnt > 0 && !c.first) {  // iteration 0 forms M = L - 0 and never reads E_old
+        const uint32_t eoff = t8_eoff(c, rc);
+#pragma unroll
+        for (int i = 0; i < K; ++i) p.eo[i] = t8_ld<kNT>(c.rE, t8_es(c, eoff, i));
+    }
+    if (c.wave == c.idwave && rc.deg > 0) {  // identity edge (a fresh streaming frame has L = ch: gen_lane)
+        p.lid = t8_ld(c.first ? c.rC : c.rL, ((uint32_t)(c.k + r) << 9) + c.lo8);
+        if (!c.first) p.eid = t8_ld<kNT>(c.rE, ((uint32_t)(rc.beg + rc.deg - 1) << 6) + c.eo8);
+    }
+}
+
+// P1: t = tanh((L[col] - E_old)/2) for this lane's slots, columns into col[];
+// returns whether some lane's own edge has |t| <= 1e-10 (:159).  Every slot is
+// evaluated (branch-free): slots past the piece hold valid data and end as 1.0.
+template <int K, bool LA>
+__device__ __forceinline__ bool t8_p1(const T8Ctx<K> &c, int r, const T8Pre<K> &pre, double (&t)[K]) {
+    bool tiny = false;
+    const int sv = t8_stage_issue(c, r + 1);
+    const T8Chunk rc = t8_chunk(c.row_ptr, r, c.wave);
+    if (rc.cnt > 0) {
+        const int nj = t8_nj(c, rc);
+        const uint16_t *lc = t8_lcols(c, r, rc);
+        const bool noE = c.first || c.fresh;  // M = L - 0 (iteration 0, :85-90)
+        double Lv[K];
+        int col[K];
+#pragma unroll
+        for (int i = 0; i < K; ++i) col[i] = lc[i];
+        if constexpr (LA) {
+#pragma unroll
+            for (int i = 0; i < K; ++i) Lv[i] = c.LA[(size_t)col[i] * kF8];
+        } else {
+            const __amdgpu_buffer_rsrc_t rs = c.first ? c.rC : c.rL;  // iteration 0: M = ch (:85-90)
+#pragma unroll
+            for (int i = 0; i < K; ++i) Lv[i] = t8_ld(rs, ((uint32_t)col[i] << 9) + c.lo8);
+        }
+#pragma unroll
+        for (int i = 0; i < K; ++i) {
+            const double M = noE ? Lv[i] : Lv[i] - pre.eo[i];  // :85-90 / :260-268
+            double th[1] = {M * 0.5};
+            np_tanh_n<1>(th, c.ttab);
+            const double tv = tanh_clip(th[0]);  // :138-146
+            tiny |= i < nj && !(fabs(tv) > kTiny);
+            t[i] = i < nj ? tv : 1.0;  // past the piece: an exact no-op in the product
+            t8_slot_fence();
+        }
+    } else {
+#pragma unroll
+        for (int i = 0; i < K; ++i) t[i] = 1.0;
+    }
+    if (c.wave == c.idwave && rc.deg > 0) {  // the identity edge: t_id, published for every P3 of row r
+        const double M = (c.first || c.fresh) ? pre.lid : pre.lid - pre.eid;
+        double th[1] = {M * 0.5};
+        np_tanh_n<1>(th, c.ttab);
+        const double tv = tanh_clip(th[0]);
+        tiny |= !(fabs(tv) > kTiny);
+        if (c.j == 0) c.slot[(kSR8 + (r & (kSR8 - 1))) * kF8] = tv;
+    }
+    t8_stage_commit(c, r + 1, sv);
+    return __ballot(tiny) != 0ull;
+}
+
+// Lane-group hand-over: group jj's value into group jj+1 (lane = group*8 + f;
+// groups 2a, 2a+1 are the halves of DPP row a).  Even jj: row_shr:8 inside the
+// row; odd jj: row_ror:8 (upper half to lower half), then row a -> a+1 by
+// v_permlane16/32_swap (tile_sub.hip group_up4).
+__device__ __forceinline__ uint32_t t8_p16(uint32_t x, int which) {
+    const auto r = __builtin_amdgcn_permlane16_swap(x, x, false, false);
+    return which ? r[1] : r[0];
+}
+__device__ __forceinline__ uint32_t t8_p32(uint32_t x, int which) {
+    const auto r = __builtin_amdgcn_permlane32_swap(x, x, false, false);
+    return which ? r[1] : r[0];
+}
+__device__ __forceinline__ uint32_t t8_up(uint32_t x, int jj) {
+    if ((jj & 1) == 0) return (uint32_t)__builtin_amdgcn_update_dpp((int)x, (int)x, 0x118, 0xf, 0xf, false);
+    x = (uint32_t)__builtin_amdgcn_update_dpp((int)x, (int)x, 0x128, 0xf, 0xf, false);
+    return (jj >> 1) == 1 ? t8_p16(t8_p32(x, 0), 1) : t8_p16(x, 0);
+}
+__device__ __forceinline__ double t8_group_up(double v, int jj) {
+    const uint64_t u = dbits(v);
+    const uint32_t lo = t8_up((uint32_t)u, jj), hi = t8_up((uint32_t)(u >> 32), jj);
+    return dfrom(((uint64_t)hi << 32) | lo);
+}
+
+// hop: this wavefront's chunk of row r's left-to-right product (:151-152).
+template <int K>
+__device__ __forceinline__ void t8_hop(T8Ctx<K> &c, int r, const double (&t)[K], bool tiny) {
+    const T8Chunk rc = t8_chunk(c.row_ptr, r, c.wave);
+    if (rc.deg == 0) return;  // spa_decoder.py:115-122
+    const int s = r & (kSR8 - 1);
+    const int ep = ((c.ep0 + r) & 0x3ffffff) * 32;
+    double *sl = c.slot + s * kF8;
+    double P = 1.0;  // 1.0 * t0 == t0 exactly
+    T8_STAMP(h0);
+    if (c.wave != 0) {
+        wait_flag<false>(c.flag + s, ep + c.wave);
+        P = *sl;
+    }
+    T8_STAMP(h1);
+    T8_ADD(c, 0, h0, h1);
+    __builtin_amdgcn_s_setprio(2);
+    if (rc.cnt > 0) {
+        // branch-free: every lane group multiplies all K slots (slots past its
+        // piece, and every slot of a group past the chunk, hold 1.0: exact
+        // no-ops), so the product ends in group 7 whatever the chunk's length
+#pragma unroll
+        for (int jj = 0; jj < kQ8; ++jj) {
+#pragma unroll
+            for (int i = 0; i < K; ++i) P = P * t[i];
+            if (jj + 1 < kQ8) P = t8_group_up(P, jj);
+        }
+    }
+    if ((threadIdx.x & 63) == 0) {
+        if (c.wave == 0)
+            lds_st(c.tinyf + s, tiny ? 1 : 0);
+        else if (tiny)
+            lds_st(c.tinyf + s, 1);
+    }
+    if (c.j == kQ8 - 1) *sl = P;
+    lds_release();
+    if ((threadIdx.x & 63) == 0) lds_st(c.flag + s, ep + c.wave + 1);
+    __builtin_amdgcn_s_setprio(0);
+    T8_STAMP(h2);
+    T8_ADD(c, 1, h1, h2);
+}
+
+// P3 of row r: E_new of this lane's slots (:159-168), stored; then, after
+// row r-1's P3 by the wavefronts whose column spans overlap this chunk's
+// (p3dep, ldpc_api.cpp sub_p3_deps: every column's additions stay rows
+// ascending), S_col += E_new; the identity column's posterior and z^1 bit.
+// p3row[v] = 1 + the last row of this pass whose P3 wavefront v finished.
+template <int K>
+__device__ __forceinline__ void t8_p3(T8Ctx<K> &c, int r, double (&t)[K]) {
+    const T8Chunk rc = t8_chunk(c.row_ptr, r, c.wave);
+    if (rc.deg == 0) {
+        if ((threadIdx.x & 63) == 0) lds_st(c.p3row + c.wave, r + 1);
+        return;
+    }
+    const int s = r & (kSR8 - 1);
+    const int ep = ((c.ep0 + r) & 0x3ffffff) * 32;
+    const bool idw = c.wave == c.idwave;  // holds the identity edge
+    double chI = 0.0;
+    if (idw) chI = t8_ld(c.rC, ((uint32_t)(c.k + r) << 9) + c.lo8);  // for L = ch + (0 + E)
+    int col[K];  // staged indices (ring row r is live until body(r + D - 1) ends)
+    {
+        const uint16_t *lc = t8_lcols(c, r, rc);
+#pragma unroll
+        for (int i = 0; i < K; ++i) col[i] = lc[i];
+    }
+    T8_STAMP(q0);
+    wait_flag<false>(c.flag + s, ep + kW8);  // row r's A product is complete
+    T8_STAMP(q1);
+    T8_ADD(c, 2, q0, q1);
+    const bool tiny_row = uniform(lds_ld(c.tinyf + s)) != 0;
+    const int nj = t8_nj(c, rc);
+    const double tI = c.slot[(kSR8 + s) * kF8];
+    const double P = c.slot[s * kF8] * tI;  // (t_0 * ... * t_{deg-2}) * t_id: left to right (:151-152)
+    double EI = 0.0;
+    if (!tiny_row) {
+        if (div_nr_ok(P)) {  // the IEEE quotient without its scaling steps (cn_common.h)
+            if (rc.cnt > 0) {
+#pragma unroll
+                for (int i = 0; i < K; ++i) {
+                    if (i < rc.CS) t[i] = 2.0 * atanh_f(clip_cl(div_nr(P, t[i])), c.ltab, c.ac);  // :159-168
+                    t8_slot_fence();
+                }
+            }
+            if (idw) EI = 2.0 * atanh_f(clip_cl(div_nr(P, tI)), c.ltab, c.ac);
+        } else {
+            if (rc.cnt > 0) {
+#pragma unroll
+                for (int i = 0; i < K; ++i)
+                    if (i < rc.CS) t[i] = 2.0 * atanh_f(clip_cl(P / t[i]), c.ltab, c.ac);
+            }
+            if (idw) EI = 2.0 * atanh_f(clip_cl(P / tI), c.ltab, c.ac);
+        }
+    } else {
+        // rare: q = in-order product of the others (np.prod(np.delete(...)),
+        // :164) for an edge with |t| <= 1e-10; t parked at row positions (the
+        // identity edge at deg-1).  Every wavefront takes part in the count.
+        const int pos0 = rc.c0 + c.j * rc.CS - rc.beg;
+        if (rc.cnt > 0) {
+#pragma unroll
+            for (int i = 0; i < K; ++i)
+                if (i < nj) c.Tb[(size_t)(pos0 + i) * kF8] = t[i];
+        }
+        if (idw && c.j == 0) c.Tb[(size_t)(rc.deg - 1) * kF8] = tI;
+        __builtin_amdgcn_s_waitcnt(0);  // scratch stores have reached L2
+        c.ntiny += 1;
+        if ((threadIdx.x & 63) == 0) __hip_atomic_fetch_add(c.tseq, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        wait_flag<false>(c.tseq, c.ntiny * kW8);
+        auto others = [&](int pos) {
+            double q = 1.0;
+            bool fst = true;
+            for (int p = 0; p < rc.deg; ++p) {
+                if (p == pos) continue;
+                const double t2 = ld_l2(c.Tb + (size_t)p * kF8);
+                q = fst ? t2 : q * t2;
+                fst = false;
+            }
+            return q;
+        };
+        if (rc.cnt > 0) {
+#pragma unroll
+            for (int i = 0; i < K; ++i) {
+                if (i < rc.CS) {
+                    const double ti = t[i];
+                    const double q = (fabs(ti) > kTiny || i >= nj) ? P / ti : others(pos0 + i);
+                    t[i] = 2.0 * atanh_f(clip_cl(q), c.ltab, c.ac);
+                }
+            }
+        }
+        if (idw) {
+            const double q = fabs(tI) > kTiny ? P / tI : others(rc.deg - 1);
+            EI = 2.0 * atanh_f(clip_cl(q), c.ltab, c.ac);
+        }
+    }
+    if (rc.cnt > 0) {  // slots past the piece (and frames that stopped) store out of range: dropped
+        const uint32_t eoff = t8_eoff(c, rc);
+#pragma unroll
+        for (int i = 0; i < K; ++i) t8_st<kNT>(c.rE, (i < nj && c.live) ? t8_es(c, eoff, i) : kOOB, t[i]);
+    }
+    if (c.live) {
+        if (idw && c.j == 0) t8_st<kNT>(c.rE, ((uint32_t)(rc.beg + rc.deg - 1) << 6) + c.eo8, EI);
+    }
+    // S order: row r-1's P3 by the overlapping wavefronts
+    T8_STAMP(q2);
+    T8_ADD(c, 3, q1, q2);
+    if (r > 0) {
+        const int d = c.p3dep[r * kW8 + c.wave];
+        for (int v = d & 0xff; v <= (d >> 8); ++v) wait_ge<false>(c.p3row + v, r);
+    }
+    T8_STAMP(q3);
+    T8_ADD(c, 4, q2, q3);
+    if (rc.cnt > 0) {
+        // S_col += E_new, rows ascending; a lane's slots never share a column
+        // within a row, so all reads, all adds, all writes (one LDS round trip)
+        double *sp[K];
+        double sv[K];
+#pragma unroll
+        for (int i = 0; i < K; ++i) sp[i] = i < nj ? c.S + (size_t)col[i] * kF8 : c.dummy;
+#pragma unroll
+        for (int i = 0; i < K; ++i) sv[i] = *sp[i];
+#pragma unroll
+        for (int i = 0; i < K; ++i) sv[i] = sv[i] + t[i];
+#pragma unroll
+        for (int i = 0; i < K; ++i) *sp[i] = sv[i];
+    }
+    if (idw && c.j == 0) {  // identity column: L = ch + (0 + E) (:173-185)
+        const double Lj = chI + (0.0 + EI);
+        if (c.live) t8_st(c.rL, ((uint32_t)(c.k + r) << 9) + c.lo8, Lj);
+        if (!(Lj < 0.0)) atomicOr(c.ib + (r >> 5) * kF8, 1u << (r & 31));
+    }
+    lds_release();  // this row's S additions before the count
+    if ((threadIdx.x & 63) == 0) lds_st(c.p3row + c.wave, r + 1);
+    T8_STAMP(q4);
+    T8_ADD(c, 5, q3, q4);
+}
+
+// body(r) with t/col buffers B (hop), B+1 mod D (P3 of row r-D+1, then P1 of r+1)
+// LA variants prefetch the next row's E_old (and identity loads) before
+// hop + P3; the L-gathering variant (8 slots per lane) has no registers for
+// that and issues them at the start of P1.
+template <int K, bool LA, int D, int B>
+__device__ __forceinline__ void t8_body(T8Ctx<K> &c, int r, double (&t)[D][K], bool (&y)[D]) {
+    constexpr int N = (B + 1) % D;
+    T8Pre<K> pre;
+    T8_STAMP(a0);
+    if (LA && r + 1 < c.m) t8_prefetch(c, r + 1, pre);
+    T8_STAMP(a1);
+    T8_ADD(c, 7, a0, a1);
+    if (r < c.m) t8_hop(c, r, t[B], y[B]);
+    if (r >= D - 1) t8_p3(c, r - (D - 1), t[N]);
+    T8_STAMP(a2);
+    if (!LA && r + 1 < c.m) t8_prefetch(c, r + 1, pre);
+    if (r + 1 < c.m) y[N] = t8_p1<K, LA>(c, r + 1, pre, t[N]);
+    T8_STAMP(a3);
+    T8_ADD(c, 6, a2, a3);
+}
+
+// One pass over all rows (every P3 done on return, before the barrier).
+template <int K, bool LA, int D>
+__device__ __forceinline__ void t8_rows(T8Ctx<K> &c) {
+    const int m = c.m;
+    double t[D][K];
+    bool y[D];
+    if (m <= 0) return;
+    {
+        t8_stage_commit(c, 0, t8_stage_issue(c, 0));
+        T8Pre<K> pre;
+        t8_prefetch(c, 0, pre);
+        y[0] = t8_p1<K, LA>(c, 0, pre, t[0]);
+    }
+    const int last = m + D - 2;  // body(last) runs P3(m-1)
+    for (int r = 0; r <= last; r += D) {
+        t8_body<K, LA, D, 0>(c, r, t, y);
+        if (r + 1 <= last) t8_body<K, LA, D, 1>(c, r + 1, t, y);
+        if constexpr (D == 3)
+            if (r + 2 <= last) t8_body<K, LA, D, 2>(c, r + 2, t, y);
+    }
+}
+
+template <int K, bool LA>
+__device__ __forceinline__ void t8_setup(T8Ctx<K> &c, unsigned char *lds, const T8Layout &ly, const DevGraph &g,
+                                         const DevState &st, int tile, int sub, const int *col_idx,
+                                         const int *row_ptr, const AtanhCoef &ac) {
+    MathLds &mlds = *(MathLds *)(lds + ly.math);
+    int *flags = (int *)(lds + ly.flags);
+    const int lane = threadIdx.x & 63;
+    c.col_idx = col_idx;
+    c.row_ptr = row_ptr;
+    c.p3dep = g.p3dep8;
+    c.wave = uniform(t8_wave(threadIdx.x >> 6));
+    c.j = lane >> 3;
+    c.f = lane & 7;
+    c.rE = t8_rsrc(st.E + (size_t)tile * g.nnz * kTile + (size_t)sub * g.nnz * kF8,
+                   ((size_t)g.nnz + kEPadEdges) * kF8 * sizeof(double));
+    c.rL = t8_rsrc(st.L + (size_t)tile * g.n * kTile, (size_t)g.n * kTile * sizeof(double));
+    c.rC = t8_rsrc(st.ch + (size_t)tile * g.n * kTile, (size_t)g.n * kTile * sizeof(double));
+    c.eo8 = (uint32_t)c.f * 8u;
+    c.lo8 = (uint32_t)(sub * kF8 + c.f) * 8u;
+    c.Tb = st.T + (size_t)blockIdx.x * g.max_row_deg * kF8 + c.f;
+    c.S = (double *)(lds + ly.S) + c.f;
+    c.LA = LA ? (double *)(lds + ly.LA) + c.f : nullptr;
+    c.dummy = (double *)(lds + ly.dummy) + c.f;
+    c.slot = (double *)(lds + ly.slot) + c.f;
+    c.ib = (uint32_t *)(lds + ly.ib) + c.f;
+    c.cidx = (uint16_t *)(lds + ly.cidx) + c.wave * kQ8 * K;
+    c.flag = flags;
+    c.tinyf = flags + kSR8;
+    c.tseq = flags + 2 * kSR8;
+    c.p3row = flags + 2 * kSR8 + 2;
+    c.ttab = LdsTanh{mlds.tanh};
+    c.ltab = LdsLog{mlds.log};
+    c.ac = ac;
+    c.m = g.m;
+    c.k = g.k;
+    c.ntiny = 0;
+    c.first = false;
+    c.fresh = false;
+    c.live = true;
+    c.ep0 = 0;
+#ifdef LDPC_T8_TIMERS
+    for (int i = 0; i < T8_NT; ++i) c.tm[i] = 0;
+#endif
+}
+
+__device__ __forceinline__ int t8_epoch0(int pass, int m) {
+    return (int)(((uint32_t)pass * (uint32_t)m) & 0x3ffffffu);
+}
+
+// End of a pass: posteriors of the A columns L = ch + S (channel added after
+// the sum, :173-185), normalized-LLR count against the previous posterior
+// (:210-228), z^1 bits; S cleared.  Thread t owns frame t & 7.
+template <bool LA>
+__device__ __forceinline__ void t8_vn(const DevGraph &g, double *S, double *LAl, uint32_t *zb, int *cntl,
+                                      const int *livel, __amdgpu_buffer_rsrc_t rL, __amdgpu_buffer_rsrc_t rC,
+                                      int sub, bool first, bool fresh_any, const int *freshl, int nllr) {
+    const int ff = threadIdx.x & 7;
+    const uint32_t lo8 = (uint32_t)(sub * kF8 + ff) * 8u;
+    const bool live = livel[ff] != 0;
+    const bool fr = fresh_any && freshl[ff] != 0;
+    int my_cnt = 0;
+    for (int e = threadIdx.x; e < g.k * kF8; e += blockDim.x) {
+        const int col = e >> 3;
+        const double Sj = S[e];
+        S[e] = 0.0;
+        const double chj = t8_ld(rC, ((uint32_t)col << 9) + lo8);
+        const double Lj = chj + Sj;
+        if (nllr) {
+            double ap;
+            if (first || fr)
+                ap = chj;
+            else if (LA)
+                ap = LAl[e];
+            else
+                ap = t8_ld(rL, ((uint32_t)col << 9) + lo8);
+            my_cnt += (fabs(Lj) <= 7.0 && ap * Lj < 0.0) ? 1 : 0;
+        }
+        if (LA) LAl[e] = Lj;
+        if (live) t8_st(rL, ((uint32_t)col << 9) + lo8, Lj);
+        if (!(Lj < 0.0)) atomicOr(zb + (col >> 5) * kF8 + ff, 1u << (col & 31));
+    }
+    if (nllr && my_cnt) atomicAdd(cntl + ff, my_cnt);
+}
+
+// syndrome (:191-204): parity of row r = popcount(A_r & (z^1)_A) + (z^1)_{k+r}
+__device__ __forceinline__ void t8_syndrome(const DevGraph &g, const uint32_t *zb, const uint32_t *ib, int *bad) {
+    const int kw = (g.k + 31) >> 5;
+    const int ff = threadIdx.x & 7;
+    uint32_t acc = 0u;
+    for (int e = threadIdx.x; e < g.m * kF8; e += blockDim.x) {
+        const int r = e >> 3;
+        const uint32_t *ar = g.a_packed + (size_t)r * kw;
+        uint32_t par = ib[(r >> 5) * kF8 + ff] >> (r & 31);
+        for (int w = 0; w < kw; ++w) par += __builtin_popcount(ar[w] & zb[w * kF8 + ff]);
+        acc |= par & 1u;
+    }
+    if (acc) atomicOr((uint32_t *)bad + ff, 1u);
+}
+
+template <int K, bool LA, int D>
+__global__ __launch_bounds__(64 * kW8, 1) void tile8_kernel(DevGraph g, DevState st, int max_iter, int nllr,
+                                                            const int *__restrict__ col_idx,
+                                                            const int *__restrict__ row_ptr, AtanhCoef ac) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+    const T8Layout ly = t8_layout(g.k, g.m, K, LA, D + 1);
+    double *S = (double *)(lds + ly.S);
+    double *LAl = LA ? (double *)(lds + ly.LA) : nullptr;
+    uint32_t *zb = (uint32_t *)(lds + ly.zb);
+    uint32_t *ib = (uint32_t *)(lds + ly.ib);
+    int *bad = (int *)(lds + ly.lane_i);
+    int *cntl = bad + kF8;
+    int *livel = cntl + kF8;
+    int *flags = (int *)(lds + ly.flags);
+    const int kw = (g.k + 31) >> 5, mw = (g.m + 31) >> 5;
+    const int tile = blockIdx.x / kQ8, sub = blockIdx.x % kQ8;
+    if (tile >= st.ntiles) return;  // block-uniform
+
+    fill_math_lds(*(MathLds *)(lds + ly.math));
+    for (int i = threadIdx.x; i < g.k * kF8; i += blockDim.x) S[i] = 0.0;
+    for (int i = threadIdx.x; i < (kw + mw) * kF8; i += blockDim.x) zb[i] = 0u;
+    for (int i = threadIdx.x; i < 2 * kF8; i += blockDim.x) bad[i] = 0;
+    if (threadIdx.x < 2 * kSR8) flags[threadIdx.x] = -1;
+    if (threadIdx.x >= 2 * kSR8 && threadIdx.x < 2 * kSR8 + 2 + kW8) flags[threadIdx.x] = 0;
+    const int lane = threadIdx.x & 63;
+    if (threadIdx.x < kF8) livel[threadIdx.x] = st.done[tile * kTile + sub * kF8 + threadIdx.x] == 0 ? 1 : 0;
+    const __amdgpu_buffer_rsrc_t rC = t8_rsrc(st.ch + (size_t)tile * g.n * kTile, (size_t)g.n * kTile * sizeof(double));
+    const __amdgpu_buffer_rsrc_t rL = t8_rsrc(st.L + (size_t)tile * g.n * kTile, (size_t)g.n * kTile * sizeof(double));
+    if constexpr (LA) {  // iteration 0 forms M = ch (:85-90): L_A starts as the channel LLRs
+        for (int e = threadIdx.x; e < g.k * kF8; e += blockDim.x)
+            LAl[e] = t8_ld(rC, ((uint32_t)(e >> 3) << 9) + (uint32_t)(sub * kF8 + (e & 7)) * 8u);
+    }
+    __syncthreads();
+    if (!st.tile_active[tile]) return;
+
+    T8Ctx<K> c;
+    t8_setup<K, LA>(c, lds, ly, g, st, tile, sub, col_idx, row_ptr, ac);
+    c.R = D + 1;
+    // the identity edge's wavefront: with D = 3 wavefront 0, which otherwise
+    // waits longest for the chain; with D = 2 the last one (wavefront 0's
+    // body would bound the row period)
+    c.idwave = D >= 3 ? 0 : kW8 - 1;
+    const int fr = tile * kTile + sub * kF8 + c.f;  // this lane's frame
+
+    for (int it = 0; it < max_iter; ++it) {
+        c.first = it == 0;
+        c.live = livel[c.f] != 0;
+        c.ep0 = t8_epoch0(it, g.m);
+        T8_STAMP(w0);
+        t8_rows<K, LA, D>(c);
+        T8_STAMP(w1);
+        T8_ADD(c, 8, w0, w1);
+        __syncthreads();  // every P3 done: S complete, identity bits set
+        if (threadIdx.x < kW8) c.p3row[threadIdx.x] = 0;
+        t8_vn<LA>(g, S, LAl, zb, cntl, livel, rL, rC, sub, c.first, false, nullptr, nllr);
+        __syncthreads();
+        t8_syndrome(g, zb, ib, bad);
+        __syncthreads();
+        if ((threadIdx.x >> 6) == 0) {  // per-frame exits, as vn_kernel (static schedule)
+            bool still = false;
+            if (lane < kF8 && c.live) {
+                if (nllr) {
+                    const int cn = cntl[lane];
+                    st.nllr_cnt[fr] = cn;
+                    if (st.nllr_hist)
+                        st.nllr_hist[(size_t)fr * st.hist_stride + it] = g.k > 0 ? (double)cn / g.k : 0.0;
+                }
+                if (bad[lane] == 0) {  // syndrome zero: Result.OK at this iteration (:231-241)
+                    st.done[fr] = 1;
+                    st.conv[fr] = it;
+                    st.status[fr] = 0;
+                    st.iters[fr] = it + 1;
+                } else if (it == max_iter - 1) {  // Result.DATA_TRANSFER_NOT_OK (:244-253)
+                    st.done[fr] = 1;
+                    st.conv[fr] = -1;
+                    st.status[fr] = 1;
+                    st.iters[fr] = it + 1;
+                } else {
+                    still = true;
+                }
+            }
+            const unsigned long long any = __ballot(still);
+            if (lane < kF8) {
+                livel[lane] = still ? 1 : 0;
+                bad[lane] = 0;
+                cntl[lane] = 0;
+            }
+            if (lane == 0) flags[2 * kSR8 + 1] = any != 0ull ? 1 : 0;
+        }
+        for (int i = threadIdx.x; i < (kw + mw) * kF8; i += blockDim.x) zb[i] = 0u;
+        __syncthreads();
+        if (!flags[2 * kSR8 + 1]) break;
+    }
+#ifdef LDPC_T8_TIMERS
+    if ((blockIdx.x == 0 || blockIdx.x == 777) && (threadIdx.x & 63) == 0)
+        printf("T8 b=%d w=%d hopw=%llu hop=%llu p3f=%llu p3m=%llu p3o=%llu p3s=%llu p1=%llu pre=%llu rows=%llu\n",
+               (int)blockIdx.x, c.wave, (unsigned long long)c.tm[0], (unsigned long long)c.tm[1],
+               (unsigned long long)c.tm[2], (unsigned long long)c.tm[3], (unsigned long long)c.tm[4],
+               (unsigned long long)c.tm[5], (unsigned long long)c.tm[6], (unsigned long long)c.tm[7],
+               (unsigned long long)c.tm[8]);
+#endif
+}
+
+// Variants: (K, L_A in LDS, pipeline depth D).  wimax_2304_0.5: (5, yes, 3);
+// the r3/4 codes: (8, no, 2) -- 8 slots per lane leave no registers for a
+// third row of t.
+constexpr int kD5 = 3, kD8 = 2;
+template <int K, bool LA, int D>
+size_t t8_lds_bytes_k(const DevGraph &g) {
+    if (!g.std_form || !g.a_packed || g.k <= 0 || g.n > 65535) return 0;
+    const int C = (g.max_row_deg + kW8 - 1) / kW8;
+    if ((C + kQ8 - 1) / kQ8 > K) return 0;
+    const size_t b = t8_layout(g.k, g.m, K, LA, D + 1).total;
+    return b <= kLds8Max ? b : 0;
+}
+
+// the variant a graph runs: 0 = none, else K * 2 + LA
+int t8_variant(const DevGraph &g) {
+    if (t8_lds_bytes_k<5, true, kD5>(g)) return 5 * 2 + 1;
+    if (t8_lds_bytes_k<8, false, kD8>(g)) return 8 * 2;
+    return 0;
+}
+
+}  // namespace
+
+int sub_frames(const DevGraph &g);  // tile_sub.hip
+
+// Whether the 8-frame decoder runs this graph (then its E is laid out in
+// 8-frame blocks, DevGraph::ef = 8; read at graph creation).  Default: the
+// codes the 16-frame sub-tile decoder cannot hold (the r3/4 codes, k = 1728);
+// wimax_2304_0.5 stays on tile_sub_kernel, measured faster.
+// LDPC_TILE8=1: every code it can run; 0: none.
+bool tile8_applies(const DevGraph &g) {
+    const char *e = getenv("LDPC_TILE8");
+    const int mode = e ? atoi(e) : -1;
+    if (mode == 0 || t8_variant(g) == 0) return false;
+    return mode == 1 || sub_frames(g) != 16;
+}
+
+size_t tile8_lds_bytes(const DevGraph &g) {
+    switch (t8_variant(g)) {
+        case 11: return t8_lds_bytes_k<5, true, kD5>(g);
+        case 16: return t8_lds_bytes_k<8, false, kD8>(g);
+        default: return 0;
+    }
+}
+
+hipError_t launch_tile8(const DevGraph &g, const DevState &st, int max_iter, bool nllr, hipStream_t s) {
+    const size_t lds = tile8_lds_bytes(g);
+    if (!lds || g.ef != kF8 || st.ntiles > st.nslots) return hipErrorInvalidValue;
+    const dim3 grid(st.ntiles * kQ8), block(64 * kW8);
+    switch (t8_variant(g)) {
+        case 11:
+            tile8_kernel<5, true, kD5><<<grid, block, lds, s>>>(g, st, max_iter, nllr ? 1 : 0, g.col_idx, g.row_ptr,
+                                                               kAtanhCoef);
+            break;
+        case 16:
+            tile8_kernel<8, false, kD8><<<grid, block, lds, s>>>(g, st, max_iter, nllr ? 1 : 0, g.col_idx,
+                                                                g.row_ptr, kAtanhCoef);
+            break;
+        default:
+            return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+}  // namespace ldpc

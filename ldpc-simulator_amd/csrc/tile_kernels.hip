@@ -673,6 +673,7 @@ static int sub_mode() {
     return e ? atoi(e) : -1;
 }
 static bool sub_enabled(const DevGraph &g) {
+    if (g.ef != kTile) return false;  // E in 8-frame blocks: tile8.hip's graph
     const int mode = sub_mode();
     if (mode == 0) return false;
     return mode == 1 || sub_frames(g) == 16;
@@ -681,11 +682,13 @@ static bool sub_enabled(const DevGraph &g) {
 size_t tile_lds_bytes(const DevGraph &g) {
     const size_t b = tile64_lds_bytes(g);
     if (b) return b;
+    if (g.ef == 8) return tile8_lds_bytes(g);
     return sub_enabled(g) ? sub_lds_bytes(g) : 0;
 }
 
 const char *tile_kernel_name(const DevGraph &g) {
     if (tile64_lds_bytes(g)) return "tile_kernel";
+    if (g.ef == 8) return tile8_lds_bytes(g) ? "tile8_kernel" : "";
     if (sub_enabled(g) && sub_lds_bytes(g)) return "tile_sub_kernel";
     return "";
 }
@@ -709,6 +712,7 @@ bool use_tile_stream(const DevGraph &g) {
     const size_t lds = tile64_lds_bytes(g);
     // + the kernel's static per-lane state (itl, freshl: 2 x 64 ints)
     if (lds) return lds + 2 * kTile * sizeof(int) <= kTileLdsMax;
+    if (g.ef == 8) return false;  // tile8.hip: static launches; streaming runs the split loop
     return sub16(g);
 }
 
@@ -728,6 +732,7 @@ hipError_t launch_tile_stream(const DevGraph &g, const DevState &st, int max_ite
 hipError_t launch_tile(const DevGraph &g, const DevState &st, int max_iter, bool nllr, hipStream_t s) {
     if (st.ntiles > st.nslots) return hipErrorInvalidValue;
     const size_t lds = tile64_lds_bytes(g);
+    if (!lds && g.ef == 8) return launch_tile8(g, st, max_iter, nllr, s);
     if (!lds) return sub_enabled(g) ? launch_tile_sub(g, st, max_iter, nllr, s) : hipErrorInvalidValue;
     tile_kernel<<<st.ntiles, 64 * kTW, lds, s>>>(g, st, max_iter, nllr ? 1 : 0, g.col_idx, g.row_ptr, kAtanhCoef);
     return hipGetLastError();

@@ -380,18 +380,28 @@ __device__ __forceinline__ void sub_hop(const SubCtx<Q> &c, int r, const double 
     }
     __builtin_amdgcn_s_setprio(2);
     int last = -1;
+    if (Q == 4 && rc.cnt > 0) {
+        // branch-free: every lane group multiplies all K slots (slots past its
+        // piece and every slot of a group past the chunk hold 1.0, sub_p1:
+        // exact no-ops), so the product ends in group 3 -- no uniform
+        // branches between the dependent multiplies
 #pragma unroll
-    for (int jj = 0; jj < Q; ++jj) {
-        if (jj * rc.CS < rc.cnt) {  // lane group jj holds edges of this chunk (uniform)
-            const double Pl = SubMul<K, K>::run(P, t, rc.CS);
-            last = jj;
-            if (jj + 1 < Q && (jj + 1) * rc.CS < rc.cnt) {
-                if (Q == 4)
-                    P = group_up4(Pl, jj);
+        for (int jj = 0; jj < Q; ++jj) {
+#pragma unroll
+            for (int i = 0; i < K; ++i) P = P * t[i];
+            if (jj + 1 < Q) P = group_up4(P, jj);
+        }
+        last = Q - 1;
+    } else {
+#pragma unroll
+        for (int jj = 0; jj < Q; ++jj) {
+            if (jj * rc.CS < rc.cnt) {  // lane group jj holds edges of this chunk (uniform)
+                const double Pl = SubMul<K, K>::run(P, t, rc.CS);
+                last = jj;
+                if (jj + 1 < Q && (jj + 1) * rc.CS < rc.cnt)
+                    P = Q == 4 ? group_up4(Pl, jj) : shfl_d(Pl, jj * F + c.f);
                 else
-                    P = shfl_d(Pl, jj * F + c.f);
-            } else {
-                P = Pl;
+                    P = Pl;
             }
         }
     }

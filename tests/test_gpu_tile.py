@@ -90,31 +90,43 @@ def test_tile_mc_counters_equal_split(gpu_available):
     np.testing.assert_array_equal(a, b)
 
 
-# --- sub-tile decoder (tile_sub.hip): the WiMAX 2304 codes, 16 or 8 frames per
-# workgroup, lane groups sharing one wavefront's chunk of a check row.  The
-# 16-frame form (wimax_2304_0.5) is the default; the 8-frame form (r3/4) is
-# opt-in (LDPC_TILE_SUB=1, read by the library at every decode)
+# --- the WiMAX 2304 codes: the 8-frame sub-tile decoder (tile8.hip, the
+# default: E in 8-frame blocks, DevGraph::ef = 8) and, with LDPC_TILE8=0 at
+# graph creation, the older 16-frame sub-tile decoder (tile_sub.hip, r1/2 only)
 
 
-@pytest.fixture
-def sub_tile(monkeypatch):
-    monkeypatch.setenv("LDPC_TILE_SUB", "1")
+def _fresh_decoder(code, frames, tile8=None, monkeypatch=None):
+    """A decoder on a NEW graph (the layout is chosen at graph creation):
+    tile8 True / False sets LDPC_TILE8=1 / 0 for it, None keeps the default."""
+    from ldpc_amd.device import Decoder, Graph
+    if tile8 is not None:
+        monkeypatch.setenv("LDPC_TILE8", "1" if tile8 else "0")
+    try:
+        return Decoder(Graph(hstd_for(code)), frames)
+    finally:
+        if tile8 is not None:
+            monkeypatch.delenv("LDPC_TILE8")
 
 
-def test_sub_tile_default_for_half_rate_opt_in_for_three_quarter(gpu_available, monkeypatch):
+def _t8(code, frames, monkeypatch):
+    """A decoder that runs tile8_kernel (wimax_2304_0.5 needs LDPC_TILE8=1)."""
+    return _fresh_decoder(code, frames, tile8=True, monkeypatch=monkeypatch)
+
+
+def test_tile8_default_for_three_quarter_codes(gpu_available, monkeypatch):
     from ldpc_amd import _lib
-    monkeypatch.delenv("LDPC_TILE_SUB", raising=False)
-    assert _lib.lib().ldpc_tile_kernel_name(_decoder("wimax_2304_0.5", 64).graph.handle) == b"tile_sub_kernel"
-    assert _lib.lib().ldpc_tile_kernel_name(_decoder("wimax_2304_0.75A", 64).graph.handle) == b""
-    monkeypatch.setenv("LDPC_TILE_SUB", "0")
-    assert _lib.lib().ldpc_tile_kernel_name(_decoder("wimax_2304_0.5", 64).graph.handle) == b""
+    name = lambda d: _lib.lib().ldpc_tile_kernel_name(d.graph.handle)  # noqa: E731
+    for code in ("wimax_2304_0.75A", "wimax_2304_0.75B"):
+        assert name(_decoder(code, 64)) == b"tile8_kernel", code
+    assert name(_decoder("wimax_2304_0.5", 64)) == b"tile_sub_kernel"
+    assert name(_decoder("wimax_576_0.5", 64)) == b"tile_kernel"
+    assert name(_t8("wimax_2304_0.5", 64, monkeypatch)) == b"tile8_kernel"
+    assert name(_fresh_decoder("wimax_2304_0.75A", 64, tile8=False, monkeypatch=monkeypatch)) == b""
 
 
-def test_sub_tile_is_the_one_launched(gpu_available, sub_tile):
-    from ldpc_amd import _lib
+def test_tile8_is_the_one_launched(gpu_available, monkeypatch):
     for code in ("wimax_2304_0.5", "wimax_2304_0.75A"):
-        dec = _decoder(code, 64)
-        assert _lib.lib().ldpc_tile_kernel_name(dec.graph.handle) == b"tile_sub_kernel"
+        dec = _t8(code, 64, monkeypatch)
         llr = _random_llr(hstd_for(code), 64, 1.0, seed=2)
         dec.profile(True)
         dec.decode(llr, 2)
@@ -124,33 +136,57 @@ def test_sub_tile_is_the_one_launched(gpu_available, sub_tile):
 
 
 @pytest.mark.parametrize("code,snr,T,B", [("wimax_2304_0.5", 0.0, 4, 70), ("wimax_2304_0.5", 3.0, 25, 40),
-                                          ("wimax_2304_0.75A", 2.0, 5, 64), ("wimax_2304_0.75B", 4.0, 8, 24)])
-def test_sub_tile_bit_identical_to_split(gpu_available, sub_tile, code, snr, T, B):
+                                          ("wimax_2304_0.5", 1.0, 50, 64),
+                                          ("wimax_2304_0.75A", 2.0, 5, 64), ("wimax_2304_0.75A", 1.0, 30, 72),
+                                          ("wimax_2304_0.75B", 4.0, 8, 24)])
+def test_tile8_bit_identical_to_split(gpu_available, monkeypatch, code, snr, T, B):
     llr = _random_llr(hstd_for(code), B, snr, seed=int(100 * snr) + 2000 + T)
-    dec = _decoder(code, B)
+    dec = _t8(code, B, monkeypatch)
     a = dec.decode(llr, T, nllr=True, post=True, hist=True, msgs=True)
     b = dec.decode(llr, T, nllr=True, post=True, hist=True, msgs=True, split=True)
     _assert_identical(a, b)
 
 
-def test_sub_tile_rare_rows_identical(gpu_available, sub_tile):
-    code = "wimax_2304_0.5"
+@pytest.mark.parametrize("code", ["wimax_2304_0.5", "wimax_2304_0.75A"])
+def test_tile8_identical_to_the_16_frame_layout(gpu_available, monkeypatch, code):
+    """E in 8-frame blocks (tile8 + its split path) == the 64-frame layout
+    (tile_sub_kernel or the split path on [tile][edge][64]), every output."""
+    llr = _random_llr(hstd_for(code), 90, 1.5, seed=77)
+    a = _t8(code, 90, monkeypatch).decode(llr, 12, nllr=True, post=True, hist=True, msgs=True)
+    b = _fresh_decoder(code, 90, tile8=False, monkeypatch=monkeypatch).decode(
+        llr, 12, nllr=True, post=True, hist=True, msgs=True)
+    _assert_identical(a, b)
+
+
+@pytest.mark.parametrize("code", ["wimax_2304_0.5", "wimax_2304_0.75A"])
+def test_tile8_rare_rows_identical(gpu_available, monkeypatch, code):
     H = hstd_for(code)
+    n = H.shape[1]
     llr = _random_llr(H, 80, 1.0, seed=19)
     llr[0, :] = 0.0
     llr[5, ::7] = 0.0
     llr[17, :] = 1e-13
     llr[66, ::3] = 0.0  # another 64-frame tile, another sub-tile
-    dec = _decoder(code, 80)
+    llr[9, : n // 2] = 0.0
+    dec = _t8(code, 80, monkeypatch)
     for T in (1, 3):
         _assert_identical(dec.decode(llr, T, nllr=True, post=True, msgs=True),
                           dec.decode(llr, T, nllr=True, post=True, msgs=True, split=True))
 
 
+def test_sub_tile16_still_identical(gpu_available, monkeypatch):
+    """The retained 16-frame sub-tile decoder (LDPC_TILE8=0) == its split path."""
+    code = "wimax_2304_0.5"
+    llr = _random_llr(hstd_for(code), 40, 3.0, seed=2025)
+    dec = _fresh_decoder(code, 40, tile8=False, monkeypatch=monkeypatch)
+    _assert_identical(dec.decode(llr, 25, nllr=True, post=True, hist=True, msgs=True),
+                      dec.decode(llr, 25, nllr=True, post=True, hist=True, msgs=True, split=True))
+
+
 @pytest.mark.parametrize("snr,T,B", [(0.0, 4, 70), (3.0, 25, 40)])
 def test_cn_row16_bit_identical_to_sub_tile(gpu_available, monkeypatch, snr, T, B):
     """The 16-wavefront x 40-edge cn_row_kernel shape (rows of wimax_2304_0.5;
-    by default only from 64 tiles on, forced here) == the sub-tile decoder."""
+    by default only from 64 tiles on, forced here) == the tile decoder."""
     code = "wimax_2304_0.5"
     llr = _random_llr(hstd_for(code), B, snr, seed=int(100 * snr) + 3000 + T)
     llr[1, ::5] = 0.0  # a rare row (|t| <= 1e-10) for cn_rare_kernel

@@ -11,7 +11,7 @@ while [ $# -ge 2 ]; do
   bd=$CS/build_$name
   rm -rf $bd; mkdir -p $bd
   objs=""
-  for f in spa_kernels.hip tile_kernels.hip tile_sub.hip frame_kernels.hip phys_kernels.hip phys_tile.hip ldpc_api.cpp hstd_builder.cpp comm.cpp; do
+  for f in $(sed -n "s/^SRCS = //p" $CS/Makefile); do
     x=""; case $f in *.cpp) x="-x hip";; esac
     /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -fno-fast-math $defs $x -c $CS/$f -o $bd/$f.o &
     objs="$objs $bd/$f.o"
