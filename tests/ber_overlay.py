@@ -15,8 +15,10 @@ iteration, and BER counts u != z^1 bits of failed frames only.
 
 Run on the GPU box:  python tests/ber_overlay.py [code]   (prints the overlay table)
 Reference curves: wimax_576_0.5 (5 points, 96-384 frames each) and the
-north-star code wimax_2304_0.5 (1.0 / 2.0 / 3.0 dB, 8 / 16 / 64 frames: a 2304
-frame-iteration costs the reference ~25 s of one core).
+north-star code wimax_2304_0.5 (1.0 / 2.0 / 3.0 dB, 8 / 80 / 64 frames: a 2304
+frame-iteration costs the reference ~25 s of one core; the 2 dB point, the only
+one off the curve's floors, is two runs of the reference summed: 16 + 64
+frames, gen_ber_curve.py --append).
 """
 import json
 import os
