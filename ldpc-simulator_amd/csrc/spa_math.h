@@ -59,6 +59,15 @@ __host__ __device__ __forceinline__ double np_tanh(double x, const Tab &tab) {
     return dfrom(dbits(r) | (ux & 0x8000000000000000ull));
 }
 
+// The check node's t = tanh(M/2) with the reference's clip (spa_decoder.py:
+// 138-146: d = M/2; d > 17.5 -> CL, d < -17.5 -> -CL, else np.tanh(d)), as
+// np_tanh of d clamped to +-17.5: np.tanh(17.5) == CL exactly and np_tanh is
+// monotone across 17.5 (tests/test_math.py), so this equals the reference for
+// every non-NaN M, and |x| <= 17.5 lets np_tanh skip its huge-argument select
+// and the output clip.
+template <class Tab>
+__host__ __device__ __forceinline__ double tanh_half_clipped(double M, const Tab &tab);
+
 // np_tanh of G independent arguments, Horner steps in lockstep across them:
 // each argument gets exactly np_tanh's operations in np_tanh's order (so the
 // results are bit-identical), but the G coefficient-table reads of a step are
@@ -96,6 +105,14 @@ __host__ __device__ __forceinline__ void np_tanh_n(double (&x)[G], const Tab &ta
         if ((ux & 0x7ff8000000000000ull) > 0x7fe0000000000000ull) v = 1.0;
         x[g] = dfrom(dbits(v) | (ux & 0x8000000000000000ull));
     }
+}
+
+template <class Tab>
+__host__ __device__ __forceinline__ double tanh_half_clipped(double M, const Tab &tab) {
+    const double d = M * 0.5;  // == M/2.0 bit for bit (power-of-two scale)
+    double x[1] = {dfrom(dbits(__builtin_fmin(__builtin_fabs(d), 17.5)) | (dbits(d) & 0x8000000000000000ull))};
+    np_tanh_n<1>(x, tab);  // |x| <= 17.5: its huge-argument select never fires
+    return x[0];
 }
 
 // ----------------------------------------------------------------- log

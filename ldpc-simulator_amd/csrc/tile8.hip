@@ -240,14 +240,14 @@ struct T8Pre {
 template <int K>
 __device__ __forceinline__ void t8_prefetch(const T8Ctx<K> &c, int r, T8Pre<K> &p) {
     const T8Chunk rc = t8_chunk(c.row_ptr, r, c.wave);
-    if (rc.cnt > 0 && !c.first) {  // iteration 0 forms M = L - 0 and never reads E_old
+    if (rc.cnt > 0) {  // iteration 0 forms M = L - 0.0 (== L exactly) and reads no E_old
         const uint32_t eoff = t8_eoff(c, rc);
 #pragma unroll
-        for (int i = 0; i < K; ++i) p.eo[i] = t8_ld<kNT>(c.rE, t8_es(c, eoff, i));
+        for (int i = 0; i < K; ++i) p.eo[i] = c.first ? 0.0 : t8_ld<kNT>(c.rE, t8_es(c, eoff, i));
     }
     if (c.wave == c.idwave && rc.deg > 0) {  // identity edge (a fresh streaming frame has L = ch: gen_lane)
         p.lid = t8_ld(c.first ? c.rC : c.rL, ((uint32_t)(c.k + r) << 9) + c.lo8);
-        if (!c.first) p.eid = t8_ld<kNT>(c.rE, ((uint32_t)(rc.beg + rc.deg - 1) << 6) + c.eo8);
+        p.eid = c.first ? 0.0 : t8_ld<kNT>(c.rE, ((uint32_t)(rc.beg + rc.deg - 1) << 6) + c.eo8);
     }
 }
 
@@ -262,7 +262,6 @@ __device__ __forceinline__ bool t8_p1(const T8Ctx<K> &c, int r, const T8Pre<K> &
     if (rc.cnt > 0) {
         const int nj = t8_nj(c, rc);
         const uint16_t *lc = t8_lcols(c, r, rc);
-        const bool noE = c.first || c.fresh;  // M = L - 0 (iteration 0, :85-90)
         double Lv[K];
         int col[K];
 #pragma unroll
@@ -277,10 +276,9 @@ __device__ __forceinline__ bool t8_p1(const T8Ctx<K> &c, int r, const T8Pre<K> &
         }
 #pragma unroll
         for (int i = 0; i < K; ++i) {
-            const double M = noE ? Lv[i] : Lv[i] - pre.eo[i];  // :85-90 / :260-268
-            double th[1] = {M * 0.5};
-            np_tanh_n<1>(th, c.ttab);
-            const double tv = tanh_clip(th[0]);  // :138-146
+            // :85-90 / :260-268 (eo = 0.0 on iteration 0; a fresh streaming frame M = L)
+            const double M = c.fresh ? Lv[i] : Lv[i] - pre.eo[i];
+            const double tv = tanh_half_clipped(M, c.ttab);  // :138-146 (spa_math.h)
             tiny |= i < nj && !(fabs(tv) > kTiny);
             t[i] = i < nj ? tv : 1.0;  // past the piece: an exact no-op in the product
             t8_slot_fence();
@@ -290,10 +288,8 @@ __device__ __forceinline__ bool t8_p1(const T8Ctx<K> &c, int r, const T8Pre<K> &
         for (int i = 0; i < K; ++i) t[i] = 1.0;
     }
     if (c.wave == c.idwave && rc.deg > 0) {  // the identity edge: t_id, published for every P3 of row r
-        const double M = (c.first || c.fresh) ? pre.lid : pre.lid - pre.eid;
-        double th[1] = {M * 0.5};
-        np_tanh_n<1>(th, c.ttab);
-        const double tv = tanh_clip(th[0]);
+        const double M = c.fresh ? pre.lid : pre.lid - pre.eid;
+        const double tv = tanh_half_clipped(M, c.ttab);
         tiny |= !(fabs(tv) > kTiny);
         if (c.j == 0) c.slot[(kSR8 + (r & (kSR8 - 1))) * kF8] = tv;
     }
@@ -701,7 +697,7 @@ __global__ __launch_bounds__(64 * kW8, 1) void tile8_kernel(DevGraph g, DevState
         __syncthreads();
         if ((threadIdx.x >> 6) == 0) {  // per-frame exits, as vn_kernel (static schedule)
             bool still = false;
-            if (lane < kF8 && c.live) {
+            if (lane < kF8 && livel[lane] != 0) {
                 if (nllr) {
                     const int cn = cntl[lane];
                     st.nllr_cnt[fr] = cn;

@@ -662,22 +662,11 @@ size_t tile64_lds_bytes(const DevGraph &g) {
     return b <= kTileLdsMax ? b : 0;
 }
 
-// The sub-tile decoder (tile_sub.hip) for the long codes.  16-frame sub-tiles
-// (wimax_2304_0.5: the north-star code) are the default -- 0.337 vs 0.31 of
-// the HBM roofline for the separate CN/VN launches at 1 dB;
-// 8-frame sub-tiles (the r3/4 codes) measured slower than the separate
-// launches and stay opt-in.  LDPC_TILE_SUB (read at every decode): 0 = never,
-// 1 = also the 8-frame form, unset = the 16-frame form only.
-static int sub_mode() {
-    const char *e = getenv("LDPC_TILE_SUB");
-    return e ? atoi(e) : -1;
-}
-static bool sub_enabled(const DevGraph &g) {
-    if (g.ef != kTile) return false;  // E in 8-frame blocks: tile8.hip's graph
-    const int mode = sub_mode();
-    if (mode == 0) return false;
-    return mode == 1 || sub_frames(g) == 16;
-}
+// The long codes: the 16-frame sub-tile decoder (tile_sub.hip) for
+// wimax_2304_0.5, the north-star code; the 8-frame decoder (tile8.hip) for
+// the r3/4 codes, whose column sums of 16 frames do not fit in LDS (their
+// graphs keep E in 8-frame blocks, DevGraph::ef = 8).
+static bool sub_enabled(const DevGraph &g) { return g.ef == kTile && sub_frames(g) == 16; }
 
 size_t tile_lds_bytes(const DevGraph &g) {
     const size_t b = tile64_lds_bytes(g);

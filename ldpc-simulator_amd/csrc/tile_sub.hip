@@ -29,8 +29,8 @@
 //
 // The default decoder of wimax_2304_0.5 (F = 16, Q = 4: the product crosses
 // lane groups with v_permlane16/32_swap); bit-identical to the split path.
-// The F = 8 form (Q = 8, ds_bpermute hand-over) for the r3/4 codes is opt-in
-// (LDPC_TILE_SUB=1): slower than the split path there.
+// (An F = 8 form of this kernel for the r3/4 codes was retired in round 3:
+// tile8.hip decodes them, with E in 8-frame blocks.)
 //
 // Per edge and iteration the HBM traffic is the algorithmic 16 B (E_old read,
 // E_new write) plus the L[col] gather (8 B, L2/MALL): the split CN/VN
@@ -104,7 +104,7 @@ constexpr int kCRing = 3;
 struct SubLayout {
     size_t S, math, slot, zb, ib, lane_i, flags, dummy, cidx, total;
 };
-__host__ __device__ constexpr int sub_k(int F) { return F == 16 ? SubCfg<4>::K : SubCfg<8>::K; }
+__host__ __device__ constexpr int sub_k(int F) { return F == 16 ? SubCfg<4>::K : 0; }
 __host__ __device__ inline SubLayout sub_layout(int k, int m, int F) {
     SubLayout t;
     size_t o = 0;
@@ -222,7 +222,7 @@ __device__ __forceinline__ uint32_t sub_eoff(const SubCtx<Q> &c, const SubChunk 
     return ((uint32_t)(rc.c0 + c.j * rc.CS) << 9) + c.lo8;
 }
 // a lane's slot i of a row chunk is at most (Q-1)*CS + K - 1 < Q*K edges past the row's end
-static_assert(4 * SubCfg<4>::K <= kEPadEdges && 8 * SubCfg<8>::K <= kEPadEdges, "E slack too small");
+static_assert(4 * SubCfg<4>::K <= kEPadEdges, "E slack too small");
 template <int Q>
 __device__ __forceinline__ double *sub_es(const SubCtx<Q> &c, uint32_t off, int i) {
     return (double *)(c.Eu + (size_t)off + (size_t)i * (kTile * sizeof(double)));
@@ -336,12 +336,6 @@ __device__ __forceinline__ double group_up4(double v, int jj) {
     return dfrom(((uint64_t)hi << 32) | lo);
 }
 
-__device__ __forceinline__ double shfl_d(double v, int src) {
-    const uint64_t u = dbits(v);
-    const int lo = __shfl((int)(uint32_t)u, src, 64);
-    const int hi = __shfl((int)(uint32_t)(u >> 32), src, 64);
-    return dfrom(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
-}
 
 // P * t[0] * ... * t[n-1] as exactly n dependent multiplies (a uniform branch
 // on n selects a straight-line sequence; slots past a lane's piece hold 1.0)
@@ -399,7 +393,7 @@ __device__ __forceinline__ void sub_hop(const SubCtx<Q> &c, int r, const double 
                 const double Pl = SubMul<K, K>::run(P, t, rc.CS);
                 last = jj;
                 if (jj + 1 < Q && (jj + 1) * rc.CS < rc.cnt)
-                    P = Q == 4 ? group_up4(Pl, jj) : shfl_d(Pl, jj * F + c.f);
+                    P = group_up4(Pl, jj);
                 else
                     P = Pl;
             }
@@ -961,17 +955,10 @@ size_t sub_lds_bytes_q(const DevGraph &g) {
 
 }  // namespace
 
-// Frames per workgroup of the sub-tile decoder for this graph: 16, 8, or 0
+// Frames per workgroup of the sub-tile decoder for this graph: 16, or 0
 // (does not apply).
-int sub_frames(const DevGraph &g) {
-    if (sub_lds_bytes_q<4>(g)) return 16;
-    if (sub_lds_bytes_q<8>(g)) return 8;
-    return 0;
-}
-size_t sub_lds_bytes(const DevGraph &g) {
-    const int F = sub_frames(g);
-    return F == 16 ? sub_lds_bytes_q<4>(g) : F == 8 ? sub_lds_bytes_q<8>(g) : 0;
-}
+int sub_frames(const DevGraph &g) { return sub_lds_bytes_q<4>(g) ? 16 : 0; }
+size_t sub_lds_bytes(const DevGraph &g) { return sub_lds_bytes_q<4>(g); }
 
 hipError_t launch_tile_sub_stream(const DevGraph &g, const DevState &st, int max_iter, bool nllr, uint64_t seed,
                                   int snr_point, double sigma, int64_t frame0, int64_t total,
@@ -987,15 +974,10 @@ hipError_t launch_tile_sub_stream(const DevGraph &g, const DevState &st, int max
 }
 
 hipError_t launch_tile_sub(const DevGraph &g, const DevState &st, int max_iter, bool nllr, hipStream_t s) {
-    const int F = sub_frames(g);
     const size_t lds = sub_lds_bytes(g);
-    if (!F || !lds) return hipErrorInvalidValue;
-    if (F == 16)
-        tile_sub_kernel<4><<<st.ntiles * 4, 64 * kSW, lds, s>>>(g, st, max_iter, nllr ? 1 : 0, g.col_idx, g.row_ptr,
-                                                                kAtanhCoef);
-    else
-        tile_sub_kernel<8><<<st.ntiles * 8, 64 * kSW, lds, s>>>(g, st, max_iter, nllr ? 1 : 0, g.col_idx, g.row_ptr,
-                                                                kAtanhCoef);
+    if (!lds) return hipErrorInvalidValue;
+    tile_sub_kernel<4><<<st.ntiles * 4, 64 * kSW, lds, s>>>(g, st, max_iter, nllr ? 1 : 0, g.col_idx, g.row_ptr,
+                                                            kAtanhCoef);
     return hipGetLastError();
 }
 

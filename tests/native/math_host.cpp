@@ -18,3 +18,7 @@ extern "C" void host_log(const double *x, double *y, long n) {
         y[i] = h + l;
     }
 }
+extern "C" void host_tanh_half_clipped(const double *m, double *y, long n) {
+    ldpc::HostTanhTab t;
+    for (long i = 0; i < n; ++i) y[i] = ldpc::tanh_half_clipped(m[i], t);
+}

@@ -72,6 +72,26 @@ def test_tanh_output_clip_equals_input_clip(host_math):
     np.testing.assert_array_equal(np.clip(y, -CL, CL).view(np.int64), sel.view(np.int64))
 
 
+def test_tanh_half_clipped_equals_reference_clip(host_math):
+    """spa_math.h tanh_half_clipped(M) (what the kernels run) == the
+    reference's d = M/2; d > 17.5 -> CL, d < -17.5 -> -CL, else np.tanh(d)
+    (spa_decoder.py:138-146), bit for bit, including -0.0 and the 2e6
+    consecutive doubles each side of +-17.5 (= M of +-35)."""
+    fn = host_math.host_tanh_half_clipped
+    fn.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_long]
+    base = np.float64(35.0).view(np.int64)
+    k = np.arange(2_000_000, dtype=np.int64)
+    rng = np.random.default_rng(12)
+    m = np.concatenate([(base + k).view(np.float64), (base - k).view(np.float64)])
+    m = np.concatenate([m, -m, rng.uniform(-80, 80, 1_000_000), rng.uniform(-2, 2, 500_000),
+                        10 ** rng.uniform(-300, 308, 200_000) * rng.choice([-1, 1], 200_000),
+                        [0.0, -0.0, 35.0, -35.0, 48.0, -48.0, 1e-320, 1.7e308, -1.7e308]])
+    d = m / 2.0
+    want = np.where(d > 17.5, CL, np.where(d < -17.5, -CL, np.tanh(d)))
+    got = _run(fn, m)
+    np.testing.assert_array_equal(got.view(np.int64), want.view(np.int64))
+
+
 def test_oracle_tanh_equals_numpy_tanh():
     import oracle
     x = _tanh_inputs(400_000, seed=9)
