@@ -841,6 +841,12 @@ int mc_stream_point(ldpc_decoder *d, uint64_t seed, int p, double sigma, int64_t
         const char *e = getenv("LDPC_COMPACT");
         return !e || atoi(e) != 0;
     }();
+    // compact once live <= cur * 64 * kc / 8 (LDPC_COMPACT_AT, eighths)
+    const int kc = [] {
+        const char *e = getenv("LDPC_COMPACT_AT");
+        return e ? std::max(1, std::min(8, atoi(e))) : 4;
+    }();
+    const bool tlog = getenv("LDPC_TAIL_LOG") != nullptr;
     for (;;) {
         // every frame fits in the slots: all start now and stop by max_iter
         const int64_t until = total <= slots ? std::max<int64_t>(step + kPoll, max_iter)
@@ -864,8 +870,10 @@ int mc_stream_point(ldpc_decoder *d, uint64_t seed, int p, double sigma, int64_t
         // tail: the supply is out and at most half of the launched slots
         // still run -> move them into the first tiles and launch only those
         const int64_t live = std::min<int64_t>((int64_t)handed, total) - (int64_t)finished;
-        if (compact && (int64_t)handed >= total && cur > 1 && live > 0 && live * 2 <= (int64_t)cur * kTile) {
-            const int nt = (int)((live + kTile - 1) / kTile);
+        if (tlog) fprintf(stderr, "[tail] step %lld cur %d live %lld\n", (long long)step, cur, (long long)live);
+        const int nt = (int)((live + kTile - 1) / kTile);
+        if (compact && (int64_t)handed >= total && cur > 1 && live > 0 && nt < cur &&
+            live * 8 <= (int64_t)cur * kTile * kc) {
             if (!d->cpairs && dev_alloc(&d->cpairs, 1 + 2 * (size_t)cap)) return LDPC_ENOMEM;
             HIP_TRY(ldpc::launch_compact(G, st, nt, cap, d->cpairs, s));
             state_bind(d, nt, nt * kTile);

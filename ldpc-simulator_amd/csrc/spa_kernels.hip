@@ -933,15 +933,18 @@ __global__ __launch_bounds__(1024) void compact_plan_kernel(DevState st, int nt,
     if (threadIdx.x == 0) pairs[0] = P;
 }
 
-// move: every (pair, item) of E / L / ch / ubits
+// move: every (item, pair) of E / L / ch / ubits.  Pair-fastest: the plan
+// lists sources and destinations in ascending slot order, so consecutive
+// threads move neighbouring lanes of one item (the lanes of a 512 B row),
+// not one lane's items 512 B apart.
 __global__ void compact_move_kernel(DevGraph g, DevState st, int cap, const int *pairs) {
     const int P = pairs[0];
     const int kw = (g.k + 31) >> 5;
     const int64_t items = (int64_t)g.nnz + 2 * (int64_t)g.n + kw;
     const int64_t total = (int64_t)P * items;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
-        const int p = (int)(i / items);
-        int64_t it = i % items;
+        const int p = (int)(i % P);
+        int64_t it = i / P;
         const int src = pairs[1 + p], dst = pairs[1 + cap + p];
         const size_t st_ = src >> 6, sl = src & 63, dt = dst >> 6, dl = dst & 63;
         if (it < g.nnz) {

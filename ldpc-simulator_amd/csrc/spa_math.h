@@ -73,7 +73,9 @@ __host__ __device__ __forceinline__ double tanh_half_clipped(double M, const Tab
 // results are bit-identical), but the G coefficient-table reads of a step are
 // independent and can be in flight together instead of one dependent read per
 // step of one chain.
-template <int G, class Tab>
+// kSmall: every |x| <= 17.5 (tanh_half_clipped): the interval index needs no
+// upper clamp and the huge-argument select never fires, so both are left out.
+template <int G, class Tab, bool kSmall = false>
 __host__ __device__ __forceinline__ void np_tanh_n(double (&x)[G], const Tab &tab) {
     int idx[G];
     double y[G], r[G], b0[G];
@@ -81,7 +83,7 @@ __host__ __device__ __forceinline__ void np_tanh_n(double (&x)[G], const Tab &ta
     for (int g = 0; g < G; ++g) {
         const uint64_t nd = dbits(x[g]) & 0x7ff8000000000000ull;
         int hi = (int)(nd >> 32) - 0x3fc00000;
-        hi = hi < 0 ? 0 : (hi > 0x780000 ? 0x780000 : hi);
+        hi = hi < 0 ? 0 : (kSmall ? hi : (hi > 0x780000 ? 0x780000 : hi));
         idx[g] = hi >> 19;
         const Pair p0 = tab(0, idx[g]);
         y[g] = __builtin_fabs(x[g]) - p0.a;
@@ -102,7 +104,7 @@ __host__ __device__ __forceinline__ void np_tanh_n(double (&x)[G], const Tab &ta
     for (int g = 0; g < G; ++g) {
         const uint64_t ux = dbits(x[g]);
         double v = __builtin_fma(r[g], y[g], b0[g]);
-        if ((ux & 0x7ff8000000000000ull) > 0x7fe0000000000000ull) v = 1.0;
+        if (!kSmall && (ux & 0x7ff8000000000000ull) > 0x7fe0000000000000ull) v = 1.0;
         x[g] = dfrom(dbits(v) | (ux & 0x8000000000000000ull));
     }
 }
@@ -111,7 +113,7 @@ template <class Tab>
 __host__ __device__ __forceinline__ double tanh_half_clipped(double M, const Tab &tab) {
     const double d = M * 0.5;  // == M/2.0 bit for bit (power-of-two scale)
     double x[1] = {dfrom(dbits(__builtin_fmin(__builtin_fabs(d), 17.5)) | (dbits(d) & 0x8000000000000000ull))};
-    np_tanh_n<1>(x, tab);  // |x| <= 17.5: its huge-argument select never fires
+    np_tanh_n<1, Tab, true>(x, tab);  // |x| <= 17.5 (17.5: interval 14 of 16)
     return x[0];
 }
 

@@ -289,15 +289,18 @@ __device__ __forceinline__ bool sub_p1(const SubCtx<Q> &c, int r, const SubChunk
                     const double M = noE ? t[i] : t[i] - eo[i];  // :85-90 / :260-268
                     d[q] = M * 0.5;
                 }
+                // :138-146 as np_tanh of M/2 clamped to +-17.5 (spa_math.h
+                // tanh_half_clipped: equal to the reference's clip for every M)
                 double th[G0];
 #pragma unroll
-                for (int q = 0; q < G0; ++q) th[q] = d[q];
-                np_tanh_n<G0>(th, c.ttab);
+                for (int q = 0; q < G0; ++q)
+                    th[q] = dfrom(dbits(fmin(fabs(d[q]), 17.5)) | (dbits(d[q]) & 0x8000000000000000ull));
+                np_tanh_n<G0, LdsTanh, true>(th, c.ttab);
 #pragma unroll
                 for (int q = 0; q < G0; ++q) {
                     const int i = g0 + q;
                     if (i < K) {
-                        const double tv = tanh_clip(th[q]);  // :138-146 (cn_common.h)
+                        const double tv = th[q];
                         tiny |= i < nj && !(fabs(tv) > kTiny);
                         // slots past this lane's piece: 1.0, an exact no-op in the chain product
                         t[i] = i < nj ? tv : 1.0;

@@ -159,13 +159,17 @@ def test_tile_stream_equals_split_stream(gpu_available, code, cap, frames, T, sn
     assert (a[:, 0] == frames).all()
 
 
-def test_stream_tail_compaction_keeps_counters(gpu_available, monkeypatch):
+@pytest.mark.parametrize("at", [None, "8"])
+def test_stream_tail_compaction_keeps_counters(gpu_available, monkeypatch, at):
     """The split streaming schedule compacts its tail (frames still running once
     the supply is out move into the first tiles): counters equal the
-    uncompacted stream and the static schedule."""
+    uncompacted stream and the static schedule -- also compacting whenever a
+    tile can be dropped (LDPC_COMPACT_AT=8)."""
     code, cap, frames, T = "wimax_2304_0.5", 256, 1500, 20
     dec = _decoder(code, cap)
     sig = [oracle.sigma_for_snr(s) for s in (2.5, 3.0)]
+    if at:
+        monkeypatch.setenv("LDPC_COMPACT_AT", at)
     a = dec.mc_run(SEED, sig, frames, 11, T, nllr=True, split=True)
     monkeypatch.setenv("LDPC_COMPACT", "0")
     b = dec.mc_run(SEED, sig, frames, 11, T, nllr=True, split=True)
