@@ -188,6 +188,12 @@ __host__ __device__ __forceinline__ double atanh_small_abs(double a, const Atanh
     return __builtin_fma(a * a2, p, a);
 }
 constexpr double kAtanhSmall = 0x1p-5;  // atanh_f's Taylor / log switch
+// Below 2^-27 the Taylor branch returns its argument: fma(a*a2, p, a) adds
+// a^3/3 < ulp(a)/6 to a, which rounds back to a.  So atanh_f(q) == q bit for
+// bit for |q| < kAtanhIdent (tests/test_math.py), and a check node whose
+// quotients are all that small (long rows at low SNR: the product of ~576
+// values of |t| < 1) forms E_new = 2q with no atanh and no clip.
+constexpr double kAtanhIdent = 0x1p-27;
 
 // atanh(q) for |q| < 2^-5 only; equals atanh_f(q) bit for bit there
 __host__ __device__ __forceinline__ double atanh_small(double q, const AtanhCoef &c = kAtanhCoef) {

@@ -441,14 +441,36 @@ __device__ __forceinline__ void sub_p3_body(SubCtx<Q> &c, int r, double (&t)[Sub
 #pragma unroll
     for (int i = 0; i < K; ++i)
         if ((BF & 2) || i < rc.CS) col[i] = lc[i];  // clamped copy past the chunk: a valid column
-    if (!tiny_row && div_nr_ok(P)) {  // the IEEE quotient without the scaling steps (cn_common.h)
+    if (!tiny_row) {
+        // q = P/t (div_nr: the IEEE quotient without the scaling steps,
+        // cn_common.h), then E_new = 2 atanh(clip(q)) (:159-168) -- or 2q when
+        // every quotient of the wavefront is below 2^-27, where that is exact
+        // (spa_math.h kAtanhIdent; the common case on long rows at low SNR)
+        bool big = false;
+        if (div_nr_ok(P)) {
 #pragma unroll
-        for (int i = 0; i < K; ++i)
-            if (i < rc.CS) t[i] = 2.0 * atanh_f(clip_cl(div_nr(P, t[i])), c.ltab, c.ac);  // :159-168
-    } else if (!tiny_row) {
+            for (int i = 0; i < K; ++i)
+                if (i < rc.CS) {
+                    t[i] = div_nr(P, t[i]);
+                    big |= !(fabs(t[i]) < kAtanhIdent);
+                }
+        } else {
 #pragma unroll
-        for (int i = 0; i < K; ++i)
-            if (i < rc.CS) t[i] = 2.0 * atanh_f(clip_cl(P / t[i]), c.ltab, c.ac);  // :159-168
+            for (int i = 0; i < K; ++i)
+                if (i < rc.CS) {
+                    t[i] = P / t[i];
+                    big |= !(fabs(t[i]) < kAtanhIdent);
+                }
+        }
+        if (__ballot(big) == 0ull) {
+#pragma unroll
+            for (int i = 0; i < K; ++i)
+                if (i < rc.CS) t[i] = 2.0 * t[i];
+        } else {
+#pragma unroll
+            for (int i = 0; i < K; ++i)
+                if (i < rc.CS) t[i] = 2.0 * atanh_f(clip_cl(t[i]), c.ltab, c.ac);
+        }
     } else {
         // rare: q = in-order product of the others (np.prod(np.delete(...)),
         // :164) for an edge with |t| <= 1e-10; t parked at row positions

@@ -119,3 +119,21 @@ def test_device_atanh_is_faithful_and_matches_numpy(host_math):
     assert np.mean(y[:: 25] == exact) > 0.99
     assert np.mean(y == np.arctanh(q)) > 0.98  # numpy (SVML) is itself ~97% CR below 0.1
     np.testing.assert_array_equal(np.signbit(y), np.signbit(q))
+
+
+def test_atanh_is_identity_below_2_pow_minus_27(host_math):
+    """spa_math.h kAtanhIdent: atanh_f(q) == q bit for bit for |q| < 2^-27 (the
+    kernels' E_new = 2q fast path for a wavefront whose quotients are all that
+    small), over the 2e6 doubles below 2^-27, log-uniform values down to the
+    subnormals, and +-0.0; and not much beyond it ([2^-26, 2^-25) already
+    holds values where it differs)."""
+    top = np.float64(2.0 ** -27).view(np.int64)
+    k = np.arange(1, 2_000_001, dtype=np.int64)
+    rng = np.random.default_rng(13)
+    q = np.concatenate([(top - k).view(np.float64), 2.0 ** rng.uniform(-1074, -27, 1_000_000),
+                        [0.0, 5e-324, 2.2250738585072014e-308]])
+    q = np.concatenate([q, -q])
+    y = _run(host_math.host_atanh, q)
+    np.testing.assert_array_equal(y.view(np.int64), q.view(np.int64))
+    w = rng.uniform(2.0 ** -26, 2.0 ** -25, 100_000)
+    assert (_run(host_math.host_atanh, w) != w).any()
