@@ -69,20 +69,12 @@ __device__ __forceinline__ void fill_math_lds(MathLds &m) {
         m.log[i] = {dfrom(tab::kLog[i][0]), dfrom(tab::kLog[i][1]), dfrom(tab::kLog[i][2]), 0.0};
 }
 
-// The +-17.5 input clip of spa_decoder.py:138-146 applied to the output:
-// np.tanh(17.5) == CL exactly and np.tanh is monotone across +-17.5, so
-//   d > 17.5 ? CL : d < -17.5 ? -CL : np.tanh(d)  ==  clip(np.tanh(d), -CL, CL)
-// for every non-NaN d (checked on the 1e8 consecutive doubles each side of
-// +-17.5 and 2.2e7 random ones up to 1e308; tests/test_math.py keeps 2e6 a
-// side): v_max_f64 + v_min_f64 instead of two
-// compares and four selects.  (NaN M: both forms give +-1 / +-CL, never the
-// reference's NaN -- out of scope, as for np_tanh.)
-__device__ __forceinline__ double tanh_clip(double th) { return clip_cl(th); }
-
-__device__ __forceinline__ double cn_tanh(double M, const LdsTanh &t) {
-    const double d = M * 0.5;  // == M/2.0 bit for bit (power-of-two scale)
-    return tanh_clip(np_tanh(d, t));  // :138-146
-}
+// t = tanh(M/2) with the reference's clip (:138-146) applied to the output:
+// np.tanh(17.5) == CL and np.tanh is monotone across +-17.5, so
+// clip(np_tanh(d), -CL, CL) is the input clip bit for bit (tests/test_math.py).
+// (The clamped-input form, spa_math.h tanh_half_clipped, has fewer VALU but
+// makes cn_row_kernel and tile_kernel spill; tile_sub.hip and tile8.hip use it.)
+__device__ __forceinline__ double cn_tanh(double M, const LdsTanh &t) { return clip_cl(np_tanh(M * 0.5, t)); }
 
 
 }  // namespace

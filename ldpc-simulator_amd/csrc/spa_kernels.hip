@@ -169,7 +169,11 @@ __global__ __launch_bounds__(256, LDPC_CN_WAVES) void cn_kernel(DevGraph g, DevS
                 const double M = es.take(k, e + k);
                 if (e + k < end) {  // wave-uniform
                     const double t = cn_tanh(M, ttab);
-                    const double En = 2.0 * atanh_f(clip_cl(nr ? div_nr(P, t) : P / t), ltab, ac);
+                    const double q = nr ? div_nr(P, t) : P / t;
+                    // 2q where exact for the whole wavefront (spa_math.h kAtanhIdent)
+                    const double En = __ballot(!(fabs(q) < kAtanhIdent)) == 0ull
+                                          ? 2.0 * q
+                                          : 2.0 * atanh_f(clip_cl(q), ltab, ac);
                     if (live) st_e(&Et[(size_t)(e + k) * g.ef], En);
                 }
             }
@@ -281,11 +285,17 @@ __global__ __launch_bounds__(64 * W, WPS) void cn_row_kernel(DevGraph g, DevStat
         __syncthreads();
     }
     const double P = chain[lane];
-    if (div_nr_ok(P)) {  // the IEEE quotient without the scaling steps (cn_common.h)
+    // q = P/t (div_nr: the IEEE quotient without the scaling steps,
+    // cn_common.h); E_new = 2 atanh(clip(q)), or 2q when every quotient of the
+    // wavefront is below 2^-27 (exact: spa_math.h kAtanhIdent), edge by edge
+    auto en = [&](double q) {
+        return __ballot(!(fabs(q) < kAtanhIdent)) == 0ull ? 2.0 * q : 2.0 * atanh_f(clip_cl(q), ltab, ac);
+    };
+    if (div_nr_ok(P)) {
 #pragma unroll
         for (int i = 0; i < K; ++i) {
             if (i < cnt) {
-                const double En = 2.0 * atanh_f(clip_cl(div_nr(P, t[i])), ltab, ac);
+                const double En = en(div_nr(P, t[i]));
                 if (live) st_e(&Et[(size_t)(c0 + i) * g.ef], En);
             }
         }
@@ -294,7 +304,7 @@ __global__ __launch_bounds__(64 * W, WPS) void cn_row_kernel(DevGraph g, DevStat
 #pragma unroll
     for (int i = 0; i < K; ++i) {
         if (i < cnt) {
-            const double En = 2.0 * atanh_f(clip_cl(P / t[i]), ltab, ac);
+            const double En = en(P / t[i]);
             if (live) st_e(&Et[(size_t)(c0 + i) * g.ef], En);
         }
     }

@@ -395,22 +395,28 @@ __device__ __forceinline__ void t8_p3(T8Ctx<K> &c, int r, double (&t)[K]) {
     const double P = c.slot[s * kF8] * tI;  // (t_0 * ... * t_{deg-2}) * t_id: left to right (:151-152)
     double EI = 0.0;
     if (!tiny_row) {
+        // q = P/t, then E_new = 2 atanh(clip(q)) (:159-168), or 2q when every
+        // quotient of the wavefront is below 2^-27 (exact: spa_math.h
+        // kAtanhIdent), decided slot by slot
+        auto en = [&](double q) {
+            return __ballot(!(fabs(q) < kAtanhIdent)) == 0ull ? 2.0 * q : 2.0 * atanh_f(clip_cl(q), c.ltab, c.ac);
+        };
         if (div_nr_ok(P)) {  // the IEEE quotient without its scaling steps (cn_common.h)
             if (rc.cnt > 0) {
 #pragma unroll
                 for (int i = 0; i < K; ++i) {
-                    if (i < rc.CS) t[i] = 2.0 * atanh_f(clip_cl(div_nr(P, t[i])), c.ltab, c.ac);  // :159-168
+                    if (i < rc.CS) t[i] = en(div_nr(P, t[i]));
                     t8_slot_fence();
                 }
             }
-            if (idw) EI = 2.0 * atanh_f(clip_cl(div_nr(P, tI)), c.ltab, c.ac);
+            if (idw) EI = en(div_nr(P, tI));
         } else {
             if (rc.cnt > 0) {
 #pragma unroll
                 for (int i = 0; i < K; ++i)
-                    if (i < rc.CS) t[i] = 2.0 * atanh_f(clip_cl(P / t[i]), c.ltab, c.ac);
+                    if (i < rc.CS) t[i] = en(P / t[i]);
             }
-            if (idw) EI = 2.0 * atanh_f(clip_cl(P / tI), c.ltab, c.ac);
+            if (idw) EI = en(P / tI);
         }
     } else {
         // rare: q = in-order product of the others (np.prod(np.delete(...)),
