@@ -109,12 +109,32 @@ __host__ __device__ __forceinline__ void np_tanh_n(double (&x)[G], const Tab &ta
     }
 }
 
+// Evaluated on a = min(|M|, 35) = 2|d| clamped (exact): np_tanh's interval of
+// a/2 is the exponent-and-top-mantissa field of a minus 2 (halving is exact
+// for the normal a of intervals >= 1; below 2^-3 both give interval 0),
+// y = |d| - b as fma(a, 0.5, -b) (one rounding either way: a*0.5 is exact
+// wherever b != 0, and b = 0 in interval 0), and the sign of M OR-ed back.
+// Same operations on the same values as np_tanh(clamped d) from the first
+// fma on, so bit-identical (tests/test_math.py), in 6 fewer VALU.  (tile8.hip
+// runs this form; tile_sub.hip keeps np_tanh_n<.., kSmall> of the clamped
+// d, which spills less there: 0.453 vs 0.437 at 1 dB.)
 template <class Tab>
 __host__ __device__ __forceinline__ double tanh_half_clipped(double M, const Tab &tab) {
-    const double d = M * 0.5;  // == M/2.0 bit for bit (power-of-two scale)
-    double x[1] = {dfrom(dbits(__builtin_fmin(__builtin_fabs(d), 17.5)) | (dbits(d) & 0x8000000000000000ull))};
-    np_tanh_n<1, Tab, true>(x, tab);  // |x| <= 17.5 (17.5: interval 14 of 16)
-    return x[0];
+    const double a = __builtin_fmin(__builtin_fabs(M), 35.0);
+    const uint32_t e = (uint32_t)(dbits(a) >> 32) >> 19;  // 12 bits: a >= 0
+    const int i = (int)__builtin_elementwise_sub_sat(e, 0x7fau);  // 0 .. 14
+    const Pair p0 = tab(0, i);
+    const double y = __builtin_fma(a, 0.5, -p0.a);
+    Pair c = tab(8, i);
+    double r = __builtin_fma(c.b, y, c.a);  // c16*y + c15
+#pragma unroll
+    for (int p = 7; p >= 1; --p) {
+        c = tab(p, i);
+        r = __builtin_fma(r, y, c.b);
+        r = __builtin_fma(r, y, c.a);
+    }
+    r = __builtin_fma(r, y, p0.b);
+    return dfrom(dbits(r) | (dbits(M) & 0x8000000000000000ull));
 }
 
 // ----------------------------------------------------------------- log
