@@ -56,7 +56,7 @@ def test_device_tanh_equals_numpy_tanh(host_math):
 
 
 def test_tanh_output_clip_equals_input_clip(host_math):
-    """cn_common.h tanh_clip: clip(np_tanh(d), -CL, CL) is the reference's
+    """cn_common.h cn_tanh: clip(np_tanh(d), -CL, CL) is the reference's
     input clip (spa_decoder.py:138-146: d > 17.5 -> CL, d < -17.5 -> -CL)
     bit for bit -- np.tanh(17.5) == CL and np_tanh is monotone across +-17.5."""
     assert np.tanh(17.5) == CL and _run(host_math.host_np_tanh, np.array([17.5]))[0] == CL
