@@ -28,6 +28,8 @@ LDPC_F_STATIC = 0x4
 LDPC_F_PHYS_HBM = 0x8
 LDPC_F_SPLIT = 0x10
 LDPC_MC_NCOUNT = 7
+LDPC_EINVAL = -22  # include/ldpc_hip.h error codes used on the Python side
+LDPC_ERANGE = -34
 
 # every symbol include/ldpc_hip.h declares
 EXPORTED = (

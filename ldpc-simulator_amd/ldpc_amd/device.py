@@ -18,8 +18,8 @@ import numpy as np
 from scipy import sparse
 
 from . import _lib
-from ._lib import (LDPC_F_DEVICE_PTRS, LDPC_F_NLLR, LDPC_F_PHYS_HBM, LDPC_F_SPLIT, LDPC_F_STATIC, LDPC_MC_NCOUNT,
-                   as_i32, check)
+from ._lib import (LDPC_EINVAL, LDPC_ERANGE, LDPC_F_DEVICE_PTRS, LDPC_F_NLLR, LDPC_F_PHYS_HBM, LDPC_F_SPLIT,
+                   LDPC_F_STATIC, LDPC_MC_NCOUNT, LdpcError, as_i32, check)
 
 
 def _csr_arrays(H):
@@ -27,6 +27,38 @@ def _csr_arrays(H):
     if not H.has_sorted_indices:
         H = H.sorted_indices()
     return H.shape[0], H.shape[1], as_i32(H.indptr), as_i32(H.indices)
+
+
+def validate_csr(m, n, indptr, indices):
+    """ldpc_graph_create's argument checks (csrc/ldpc_api.cpp), HIP-free, so a
+    bad H fails where it is handed over (SPA_Decoder.__init__ in the parent
+    process, as the reference's constructor would) rather than on the first
+    decode() inside a forked worker.  Raises LdpcError with the C codes."""
+    fn = "ldpc_graph_create"
+    if m <= 0 or n <= 0 or m > n:
+        raise LdpcError(fn, LDPC_EINVAL, f"bad shape m={m} n={n}")
+    indptr = np.asarray(indptr)
+    indices = np.asarray(indices)
+    if len(indptr) != m + 1 or indptr[0] != 0:
+        raise LdpcError(fn, LDPC_EINVAL, "row_ptr[0] != 0")
+    nnz = int(indptr[-1])
+    lim = (2 ** 31 - 1) // 64  # within-tile offsets are 32-bit: e * 64 must fit
+    if nnz <= 0 or nnz > lim or n > lim:
+        raise LdpcError(fn, LDPC_ERANGE, f"nnz={nnz} outside 32-bit tile indexing")
+    d = np.diff(indptr)
+    if (d < 0).any():
+        raise LdpcError(fn, LDPC_EINVAL, f"row_ptr not monotone at {int(np.argmax(d < 0))}")
+    if len(indices) < nnz or (indices[:nnz] < 0).any() or (indices[:nnz] >= n).any():
+        raise LdpcError(fn, LDPC_EINVAL, "column out of range")
+    c = indices[:nnz].astype(np.int64)
+    step = np.diff(c)
+    same_row = np.ones(max(nnz - 1, 0), bool)
+    same_row[(indptr[1:-1][(indptr[1:-1] > 0) & (indptr[1:-1] < nnz)] - 1)] = False
+    bad = (step <= 0) & same_row
+    if bad.any():
+        r = int(np.searchsorted(indptr, int(np.argmax(bad)) + 1, side="right") - 1)
+        raise LdpcError(fn, LDPC_EINVAL, f"row {r} columns not strictly ascending "
+                                         "(the reference's check_to_var order is required)")
 
 
 class Graph:

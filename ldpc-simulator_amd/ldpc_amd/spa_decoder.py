@@ -4,7 +4,10 @@ Same constructor and call as python_ldpc_app/spa_decoder.py:
     SPA_Decoder(encoder_decoder_data, settings)            (:16-42)
     decode(data_buffer) -> Result                          (:63-280)
 Construction does no HIP work: the graph upload and the device workspace are
-made by the first decode() in the process that calls it.  main.py:221 builds
+made by the first decode() in the process that calls it.  It does validate H
+(ldpc_graph_create's checks, HIP-free), so a malformed matrix fails in the
+constructor, as in the reference; a bad device or an HBM shortfall surfaces
+on the first decode().  main.py:221 builds
 a decoder in the parent and then forks a ProcessPoolExecutor whose workers
 build their own (main.py:78, main.py:248-256; adaptive.py:227-282): the
 parent never starts HIP, each worker starts its own (ldpc_amd._lib.gpu).
@@ -24,7 +27,7 @@ import os
 import numpy as np
 from scipy import sparse
 
-from .device import Decoder, Graph
+from .device import Decoder, Graph, _csr_arrays, validate_csr
 from .enums import caller_result_enum
 
 
@@ -50,6 +53,14 @@ class SPA_Decoder:
         if H.shape != (encoder_decoder_data._m, encoder_decoder_data._n):
             raise ValueError(f"H_std shape {H.shape} != (m, n) = "
                              f"({encoder_decoder_data._m}, {encoder_decoder_data._n})")
+        # fail fast, HIP-free: the graph checks of ldpc_graph_create and the
+        # argument ranges (the device itself is first touched by decode())
+        _, _, indptr, indices = _csr_arrays(H)
+        validate_csr(H.shape[0], H.shape[1], indptr, indices)
+        if int(device) < -1:
+            raise ValueError(f"device index {device} < -1")
+        if int(max_frames) < 1:
+            raise ValueError(f"max_frames {max_frames} < 1")
         self.H_sparse = H
         self._device_index = device
         self._max_frames = max_frames
