@@ -82,10 +82,18 @@ constexpr int kSG = 1;
 // lane's slots never share a column within a row; +1.1 %, profiles r2z logs).
 // Template flag BF selects these forms per kernel: bit 0 the branch-free P1,
 // bit 1 the branch-free P3 (clamped column reads, batched S updates).  The
-// streaming kernel (more live refill state, more spills) gains from bit 0
-// (+3.4 % at 2 dB) but loses 8 % to bit 1 (profiles/r2ag_stream_bf).
-constexpr int kStaticBF = 3;
-constexpr int kStreamBF = 1;
+// streaming kernel (more live refill state, more spills) took bit 0 only in
+// round 2 (profiles/r2ag_stream_bf); since the round-3 math trims bit 1 alone
+// is its best form: 2 dB 6.88k (bit 0) / 7.10k (both) / 7.12k (neither) /
+// 7.28k cw/s (bit 1) (profiles/r3_ab/ab_sbf).
+#ifndef SUB_STATIC_BF
+#define SUB_STATIC_BF 3
+#endif
+constexpr int kStaticBF = SUB_STATIC_BF;
+#ifndef SUB_STREAM_BF
+#define SUB_STREAM_BF 2
+#endif
+constexpr int kStreamBF = SUB_STREAM_BF;
 // Logical wavefront (chunk position in a row) of hardware wavefront hw: the
 // four wavefronts of one SIMD (hw = s, s+4, s+8, s+12) take four consecutive
 // chunk positions, so each SIMD holds one contiguous quarter of every row's

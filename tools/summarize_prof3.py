@@ -70,6 +70,11 @@ def main(src, dst, nnz, frames, iters, fps):
         "slot_definition": "one wavefront instruction over 64 lanes = %d edges x %d frames" % (64 // fps, fps),
     }
     json.dump(out, open(os.path.join(dst, "summary.json"), "w"), indent=1)
+    # bench.py committed_traffic(): HBM bytes per launch of this exact shape
+    json.dump({"edges": nnz, "frames": frames, "source": "summary.json (this directory)",
+               "kernels": {"tile": {"kernel": dk, "traffic_bytes": rd + wr, "read_bytes": rd, "write_bytes": wr,
+                                    "avg_ns": out["avg_ms"] * 1e6}}},
+              open(os.path.join(dst, "traffic.json"), "w"), indent=1)
     print(json.dumps({k: v for k, v in out.items() if k != "sq_T10"}, indent=1))
     print(json.dumps({k: v for k, v in out["sq_T10"].items() if k != "SQ"}, indent=1))
 
