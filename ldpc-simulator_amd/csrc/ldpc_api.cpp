@@ -253,6 +253,40 @@ hipError_t timed(ldpc_decoder *d, int kind, hipStream_t s, F &&fn) {
     return e;
 }
 
+bool tail_vn_enabled();
+
+// Few tiles of a long-row code: the per-tile vn_kernel (one workgroup per
+// tile: ~11 ms a pass) and the sub-tile decoders (one workgroup per 16 or 8
+// frames: ~11 / ~6 ms a pass whatever the frame count) are latency-bound there,
+// while the split CN + the column-parallel VN (vn_cols_kernel +
+// tail_exit_kernel<true>) spread a pass over the chip (~0.3 ms per tile) --
+// the drop-in per-frame decode() path (64 slots): one wimax_2304_0.5 frame at
+// T=50 in 100 ms instead of 746 ms (tools/probe_decode_latency.py, profiles/
+// r3_ab/scols2).  LDPC_SMALL_COLS (read per call): the tile count up to which
+// it applies (default: 32 for the 16-frame sub-tile codes, 16 for tile8's
+// -- the measured cross-overs; 0 = never).
+bool small_batch_cols(const DevGraph &G, int ntiles) {
+    if (!G.a_packed || ((G.k + 31) >> 5) > 64 || !tail_vn_enabled()) return false;
+    const char *e = getenv("LDPC_SMALL_COLS");
+    const int lim = e ? atoi(e) : (G.ef == 8 ? 16 : 32);
+    if (ntiles > lim) return false;
+    return !ldpc::use_tile(G) || ldpc::sub_frames(G) == 16 || G.ef == 8;
+}
+
+// the column-parallel VN's per-tile buffers (zero between passes)
+int ensure_tail_bufs(ldpc_decoder *d, hipStream_t s) {
+    const DevGraph &G = d->g->dg;
+    const int cap = d->cap_tiles * kTile;
+    const size_t nzb = (size_t)d->cap_tiles * ((G.n + 31) / 32) * kTile;
+    if (!d->tzb && (dev_alloc(&d->tzb, nzb) || dev_alloc(&d->tcnt, (size_t)cap))) return LDPC_ENOMEM;
+    // tail_exit_kernel leaves them zero, but a call that stopped early (an
+    // error return) may not have: cleared per call, never trusted
+    if (hipMemsetAsync(d->tzb, 0, nzb * sizeof(uint32_t), s) != hipSuccess ||
+        hipMemsetAsync(d->tcnt, 0, (size_t)cap * sizeof(int), s) != hipSuccess)
+        return ldpc_fail(LDPC_EDEVICE, "tail buffers: memset failed");
+    return LDPC_OK;
+}
+
 // Up to max_iter CN/VN sweeps.  With poll (callers that synchronise anyway),
 // the host reads how many tiles are still running after VN(it) for it < 4 and
 // every 4th iteration after, and stops once none is: launches over finished
@@ -261,7 +295,8 @@ hipError_t run_iterations(ldpc_decoder *d, const DevGraph &G, const DevState &st
                           hipStream_t s, bool poll, bool split) {
     hipError_t e = hipSuccess;
     DevState st = st_in;
-    if (!split && ldpc::use_tile(G) && st.ntiles <= st.nslots)  // one launch: every tile runs to its own exit
+    const bool cols = small_batch_cols(G, st.ntiles) && ensure_tail_bufs(d, s) == LDPC_OK;
+    if (!split && !cols && ldpc::use_tile(G) && st.ntiles <= st.nslots)  // one launch: every tile to its own exit
         return timed(d, LDPC_K_TILE, s, [&] { return ldpc::launch_tile(G, st, max_iter, nllr, s); });
     // cn_rare_kernel clears the OTHER parity's count for the next CN; the one
     // the last iteration used (or an early stop left) is cleared here
@@ -281,7 +316,10 @@ hipError_t run_iterations(ldpc_decoder *d, const DevGraph &G, const DevState &st
         e = timed(d, LDPC_K_CN, s, [&] { return ldpc::launch_cn(G, st, it, s); });
         if (e == hipSuccess) e = ldpc::launch_cn_rare(G, st, it, s);
         if (e == hipSuccess)
-            e = timed(d, LDPC_K_VN, s, [&] { return ldpc::launch_vn(G, st, it, max_iter, nllr, s); });
+            e = timed(d, LDPC_K_VN, s, [&] {
+                return cols ? ldpc::launch_vn_cols_decode(G, st, it, it + 1 == max_iter, nllr, d->tzb, d->tcnt, s)
+                            : ldpc::launch_vn(G, st, it, max_iter, nllr, s);
+            });
         if (e == hipSuccess && poll && it + 1 < max_iter && (it < 4 || (it + 1) % 4 == 0)) {
             int running = 0;
             e = hipMemcpyAsync(&running, d->pactive + it, sizeof(int), hipMemcpyDeviceToHost, s);
@@ -787,14 +825,8 @@ int mc_stream_point(ldpc_decoder *d, uint64_t seed, int p, double sigma, int64_t
     const int cap = d->cap_tiles * kTile;
     // streaming tail VN (column-parallel, launch_vn_tail) once few tiles run
     const bool tail_ok = G.a_packed && ((G.k + 31) >> 5) <= 64 && tail_vn_enabled();
-    if (tail_ok) {
-        const size_t nzb = (size_t)d->cap_tiles * ((G.n + 31) / 32) * kTile;
-        if (!d->tzb && (dev_alloc(&d->tzb, nzb) || dev_alloc(&d->tcnt, (size_t)cap))) return LDPC_ENOMEM;
-        // tail_exit_kernel leaves them zero, but a point that stopped early (an
-        // error return) may not have: cleared per point, never trusted
-        HIP_TRY(hipMemsetAsync(d->tzb, 0, nzb * sizeof(uint32_t), s));
-        HIP_TRY(hipMemsetAsync(d->tcnt, 0, (size_t)cap * sizeof(int), s));
-    }
+    if (tail_ok)
+        if (int rc = ensure_tail_bufs(d, s)) return rc;
     auto refill = [&] {
         return timed(d, LDPC_K_GEN, s,
                      [&] { return ldpc::launch_refill(G, st, seed, p, sigma, frame0, total, next, s); });

@@ -127,6 +127,8 @@ hipError_t launch_stream_init(const DevGraph &g, const DevState &st, hipStream_t
 // (left zero on exit); std_form graphs with k <= 2048
 hipError_t launch_vn_tail(const DevGraph &g, const DevState &st, int max_iter, bool nllr, uint32_t *zb, int *cnt,
                           unsigned long long *ctr, hipStream_t s);
+hipError_t launch_vn_cols_decode(const DevGraph &g, const DevState &st, int it, bool last, bool nllr, uint32_t *zb,
+                                 int *cnt, hipStream_t s);
 hipError_t launch_refill(const DevGraph &g, const DevState &st, uint64_t seed, int snr_point, double sigma,
                          int64_t frame0, int64_t total, unsigned long long *next, hipStream_t s);
 // streaming tail: move the frames running in tiles >= nt into finished slots

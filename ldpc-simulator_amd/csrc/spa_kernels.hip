@@ -152,7 +152,7 @@ __global__ __launch_bounds__(256, LDPC_CN_WAVES) void cn_kernel(DevGraph g, DevS
                 if (e + k < end) {  // wave-uniform
                     const double t = cn_tanh(M, ttab);
                     P = (e + k == beg) ? t : P * t;
-                    tiny |= !(fabs(t) > kTiny);
+                    tiny |= live && !(fabs(t) > kTiny);  // a frame-less lane never votes
                 }
             }
         }
@@ -162,7 +162,8 @@ __global__ __launch_bounds__(256, LDPC_CN_WAVES) void cn_kernel(DevGraph g, DevS
         // E_new = 2 atanh(clip(P/t)) written over E_old.  24 B of HBM per edge
         // instead of parking t (32 B).
         EdgeStream<kFirst, kStream> es(col_idx, Lt, Et, beg, end, fresh, g.ef);
-        const bool nr = div_nr_ok(P);  // wave-uniform (cn_common.h)
+        const bool nr = div_nr_ok(live ? P : 1.0);  // wave-uniform (cn_common.h); frame-less lanes do not vote
+        const double lim = live ? kAtanhIdent : INFINITY;
         for (int e = beg; e < end; e += kPf) {
 #pragma unroll
             for (int k = 0; k < kPf; ++k) {
@@ -171,7 +172,7 @@ __global__ __launch_bounds__(256, LDPC_CN_WAVES) void cn_kernel(DevGraph g, DevS
                     const double t = cn_tanh(M, ttab);
                     const double q = nr ? div_nr(P, t) : P / t;
                     // 2q where exact for the whole wavefront (spa_math.h kAtanhIdent)
-                    const double En = __ballot(!(fabs(q) < kAtanhIdent)) == 0ull
+                    const double En = __ballot(!(fabs(q) < lim)) == 0ull
                                           ? 2.0 * q
                                           : 2.0 * atanh_f(clip_cl(q), ltab, ac);
                     if (live) st_e(&Et[(size_t)(e + k) * g.ef], En);
@@ -262,7 +263,7 @@ __global__ __launch_bounds__(64 * W, WPS) void cn_row_kernel(DevGraph g, DevStat
                 if (i < cnt) {
                     const double M = kFirst ? t[i] : t[i] - ((kStream && fresh) ? 0.0 : eo[i - h * H]);
                     t[i] = cn_tanh(M, ttab);
-                    tiny |= !(fabs(t[i]) > kTiny);
+                    tiny |= live && !(fabs(t[i]) > kTiny);
                 }
             }
         }
@@ -288,10 +289,11 @@ __global__ __launch_bounds__(64 * W, WPS) void cn_row_kernel(DevGraph g, DevStat
     // q = P/t (div_nr: the IEEE quotient without the scaling steps,
     // cn_common.h); E_new = 2 atanh(clip(q)), or 2q when every quotient of the
     // wavefront is below 2^-27 (exact: spa_math.h kAtanhIdent), edge by edge
+    const double lim = live ? kAtanhIdent : INFINITY;  // frame-less lanes do not vote
     auto en = [&](double q) {
-        return __ballot(!(fabs(q) < kAtanhIdent)) == 0ull ? 2.0 * q : 2.0 * atanh_f(clip_cl(q), ltab, ac);
+        return __ballot(!(fabs(q) < lim)) == 0ull ? 2.0 * q : 2.0 * atanh_f(clip_cl(q), ltab, ac);
     };
-    if (div_nr_ok(P)) {
+    if (div_nr_ok(live ? P : 1.0)) {
 #pragma unroll
         for (int i = 0; i < K; ++i) {
             if (i < cnt) {
@@ -516,7 +518,8 @@ __global__ __launch_bounds__(1024) void vn_kernel(DevGraph g, DevState st, int i
 // vn_kernel<.., kStream>'s per-frame exits and counters (main.py:130-138).
 // zb and cnt are all-zero between iterations (tail_exit clears its tile).
 constexpr int kTv = 16;
-__global__ __launch_bounds__(256) void vn_cols_kernel(DevGraph g, DevState st, int nllr, uint32_t *zb, int *cnt) {
+__global__ __launch_bounds__(256) void vn_cols_kernel(DevGraph g, DevState st, int nllr, uint32_t *zb, int *cnt,
+                                                      int first) {
     const int tile = blockIdx.y;
     const int j = blockIdx.x * 4 + (int)(threadIdx.x >> 6);  // column (uniform per wavefront)
     if (j >= g.n || !st.tile_active[tile]) return;
@@ -541,7 +544,9 @@ __global__ __launch_bounds__(256) void vn_cols_kernel(DevGraph g, DevState st, i
     const double chj = st.ch[ci];
     const double Lj = chj + s;  // channel added after the sum
     if (nllr && j < g.k) {
-        const double ap = st.L[ci];  // previous posterior (= ch on a frame's first pass)
+        // previous posterior: ch on iteration 0 of a decode (L not yet written,
+        // vn_kernel<true>), L = ch on a streaming frame's first pass
+        const double ap = first ? chj : st.L[ci];
         if (fabs(Lj) <= 7.0 && ap * Lj < 0.0) atomicAdd(&cnt[f], 1);
     }
     if (live) st.L[ci] = Lj;
@@ -553,8 +558,13 @@ __global__ __launch_bounds__(256) void vn_cols_kernel(DevGraph g, DevState st, i
 
 constexpr int kTailWaves = 16;
 constexpr int kTailKw = 64;  // (z^1)_A words held per lane: k <= 2048
-__global__ __launch_bounds__(64 * kTailWaves) void tail_exit_kernel(DevGraph g, DevState st, int last, int nllr,
-                                                                     uint32_t *zb, int *cnt,
+// kDecode (ldpc_decode_f64 on few tiles, run_iterations): `it` is the pass,
+// `last` whether it is the final one, and the exits are vn_kernel<.., false>'s
+// (conv / status / iters, the normalized-LLR history, the host poll's count);
+// otherwise `last` is max_iter and the exits are the streaming ones.
+template <bool kDecode>
+__global__ __launch_bounds__(64 * kTailWaves) void tail_exit_kernel(DevGraph g, DevState st, int it, int last,
+                                                                     int nllr, uint32_t *zb, int *cnt,
                                                                      unsigned long long *ctr) {
     __shared__ int bad[kTile];
     const int tile = blockIdx.x;
@@ -585,7 +595,37 @@ __global__ __launch_bounds__(64 * kTailWaves) void tail_exit_kernel(DevGraph g, 
     }
     if (acc) atomicOr(&bad[lane], 1);
     __syncthreads();
-    if (wave == 0) {  // vn_kernel<false, true>'s exits and counters
+    if (kDecode && wave == 0) {  // vn_kernel<.., false>'s exits
+        const bool live = st.done[f] == 0;
+        bool still = false;
+        if (live) {
+            if (nllr) {
+                const int c = cnt[f];
+                st.nllr_cnt[f] = c;
+                if (st.nllr_hist) st.nllr_hist[(size_t)f * st.hist_stride + it] = g.k > 0 ? (double)c / g.k : 0.0;
+            }
+            if (bad[lane] == 0) {  // syndrome zero: Result.OK at this iteration
+                st.done[f] = 1;
+                st.conv[f] = it;
+                st.status[f] = 0;
+                st.iters[f] = it + 1;
+            } else if (last) {  // Result.DATA_TRANSFER_NOT_OK
+                st.done[f] = 1;
+                st.conv[f] = -1;
+                st.status[f] = 1;
+                st.iters[f] = it + 1;
+            } else {
+                still = true;
+            }
+        }
+        const unsigned long long any = __ballot(still);
+        if (lane == 0) {
+            st.tile_active[tile] = any != 0ull ? 1 : 0;
+            if (any && st.active_count) atomicAdd(&st.active_count[it], 1);  // host poll: 0 -> all stopped
+        }
+        cnt[f] = 0;
+    }
+    if (!kDecode && wave == 0) {  // vn_kernel<false, true>'s exits and counters
         const bool live = st.done[f] == 0;
         const int itl = st.iters[f];
         const bool lastl = itl == last - 1;
@@ -880,8 +920,20 @@ hipError_t launch_vn(const DevGraph &g, const DevState &st, int it, int max_iter
 hipError_t launch_vn_tail(const DevGraph &g, const DevState &st, int max_iter, bool nllr, uint32_t *zb, int *cnt,
                           unsigned long long *ctr, hipStream_t s) {
     if (!g.a_packed || !st.ubits || ((g.k + 31) >> 5) > kTailKw) return hipErrorInvalidValue;
-    vn_cols_kernel<<<dim3((unsigned)((g.n + 3) / 4), (unsigned)st.ntiles), 256, 0, s>>>(g, st, nllr ? 1 : 0, zb, cnt);
-    tail_exit_kernel<<<st.ntiles, 64 * kTailWaves, 0, s>>>(g, st, max_iter, nllr ? 1 : 0, zb, cnt, ctr);
+    vn_cols_kernel<<<dim3((unsigned)((g.n + 3) / 4), (unsigned)st.ntiles), 256, 0, s>>>(g, st, nllr ? 1 : 0, zb, cnt,
+                                                                                      0);
+    tail_exit_kernel<false><<<st.ntiles, 64 * kTailWaves, 0, s>>>(g, st, 0, max_iter, nllr ? 1 : 0, zb, cnt, ctr);
+    return hipGetLastError();
+}
+
+// ldpc_decode_f64 on few tiles: pass `it` of the column-parallel VN
+hipError_t launch_vn_cols_decode(const DevGraph &g, const DevState &st, int it, bool last, bool nllr, uint32_t *zb,
+                                 int *cnt, hipStream_t s) {
+    if (!g.a_packed || ((g.k + 31) >> 5) > kTailKw) return hipErrorInvalidValue;
+    vn_cols_kernel<<<dim3((unsigned)((g.n + 3) / 4), (unsigned)st.ntiles), 256, 0, s>>>(g, st, nllr ? 1 : 0, zb, cnt,
+                                                                                      it == 0 ? 1 : 0);
+    tail_exit_kernel<true><<<st.ntiles, 64 * kTailWaves, 0, s>>>(g, st, it, last ? 1 : 0, nllr ? 1 : 0, zb, cnt,
+                                                                 nullptr);
     return hipGetLastError();
 }
 

@@ -261,6 +261,7 @@ __device__ __forceinline__ bool t8_p1(const T8Ctx<K> &c, int r, const T8Pre<K> &
     const T8Chunk rc = t8_chunk(c.row_ptr, r, c.wave);
     if (rc.cnt > 0) {
         const int nj = t8_nj(c, rc);
+        const int njt = c.live ? nj : 0;  // the |t| <= 1e-10 vote: frame-less lanes abstain
         const uint16_t *lc = t8_lcols(c, r, rc);
         double Lv[K];
         int col[K];
@@ -279,7 +280,7 @@ __device__ __forceinline__ bool t8_p1(const T8Ctx<K> &c, int r, const T8Pre<K> &
             // :85-90 / :260-268 (eo = 0.0 on iteration 0; a fresh streaming frame M = L)
             const double M = c.fresh ? Lv[i] : Lv[i] - pre.eo[i];
             const double tv = tanh_half_clipped(M, c.ttab);  // :138-146 (spa_math.h)
-            tiny |= i < nj && !(fabs(tv) > kTiny);
+            tiny |= i < njt && !(fabs(tv) > kTiny);
             t[i] = i < nj ? tv : 1.0;  // past the piece: an exact no-op in the product
             t8_slot_fence();
         }
@@ -290,7 +291,7 @@ __device__ __forceinline__ bool t8_p1(const T8Ctx<K> &c, int r, const T8Pre<K> &
     if (c.wave == c.idwave && rc.deg > 0) {  // the identity edge: t_id, published for every P3 of row r
         const double M = c.fresh ? pre.lid : pre.lid - pre.eid;
         const double tv = tanh_half_clipped(M, c.ttab);
-        tiny |= !(fabs(tv) > kTiny);
+        tiny |= c.live && !(fabs(tv) > kTiny);
         if (c.j == 0) c.slot[(kSR8 + (r & (kSR8 - 1))) * kF8] = tv;
     }
     t8_stage_commit(c, r + 1, sv);
@@ -398,10 +399,11 @@ __device__ __forceinline__ void t8_p3(T8Ctx<K> &c, int r, double (&t)[K]) {
         // q = P/t, then E_new = 2 atanh(clip(q)) (:159-168), or 2q when every
         // quotient of the wavefront is below 2^-27 (exact: spa_math.h
         // kAtanhIdent), decided slot by slot
+        const double lim = c.live ? kAtanhIdent : INFINITY;  // frame-less lanes do not vote
         auto en = [&](double q) {
-            return __ballot(!(fabs(q) < kAtanhIdent)) == 0ull ? 2.0 * q : 2.0 * atanh_f(clip_cl(q), c.ltab, c.ac);
+            return __ballot(!(fabs(q) < lim)) == 0ull ? 2.0 * q : 2.0 * atanh_f(clip_cl(q), c.ltab, c.ac);
         };
-        if (div_nr_ok(P)) {  // the IEEE quotient without its scaling steps (cn_common.h)
+        if (div_nr_ok(c.live ? P : 1.0)) {  // the IEEE quotient without its scaling steps (cn_common.h)
             if (rc.cnt > 0) {
 #pragma unroll
                 for (int i = 0; i < K; ++i) {

@@ -156,7 +156,7 @@ __device__ __forceinline__ bool tile_t(const TileCtx &c, double &t, double eo) {
     // clamped-input form, tanh_half_clipped, spills here and measured 26 %
     // slower on wimax_576_0.5)
     t = clip_cl(np_tanh(M * 0.5, c.ttab));  // :138-146 (tests/test_math.py: output clip == input clip)
-    return !(fabs(t) > kTiny);
+    return c.live && !(fabs(t) > kTiny);  // a frame-less lane never votes
 }
 
 // P1: loads of the chunk, then t = tanh((L - E_old)/2) edge by edge; returns

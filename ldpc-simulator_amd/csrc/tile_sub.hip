@@ -83,17 +83,21 @@ constexpr int kSG = 1;
 // Template flag BF selects these forms per kernel: bit 0 the branch-free P1,
 // bit 1 the branch-free P3 (clamped column reads, batched S updates).  The
 // streaming kernel (more live refill state, more spills) took bit 0 only in
-// round 2 (profiles/r2ag_stream_bf); since the round-3 math trims bit 1 alone
-// is its best form: 2 dB 6.88k (bit 0) / 7.10k (both) / 7.12k (neither) /
-// 7.28k cw/s (bit 1) (profiles/r3_ab/ab_sbf).
+// round 2 (profiles/r2ag_stream_bf); since the round-3 math trims both bits
+// are its best valid form: 2 dB 6.88k (bit 0) vs 7.10k cw/s (both)
+// (profiles/r3_ab/ab_sbf; forms without bit 0 leave the padded slots unset
+// for the branch-free hop: wrong products, caught by
+// tests/test_gpu_config3.py's stream == static check).
 #ifndef SUB_STATIC_BF
 #define SUB_STATIC_BF 3
 #endif
 constexpr int kStaticBF = SUB_STATIC_BF;
 #ifndef SUB_STREAM_BF
-#define SUB_STREAM_BF 2
+#define SUB_STREAM_BF 3
 #endif
 constexpr int kStreamBF = SUB_STREAM_BF;
+// the branch-free hop (Q = 4) multiplies all K slots: P1 must pad them (bit 0)
+static_assert((kStaticBF & 1) && (kStreamBF & 1), "the branch-free hop needs the branch-free P1");
 // Logical wavefront (chunk position in a row) of hardware wavefront hw: the
 // four wavefronts of one SIMD (hw = s, s+4, s+8, s+12) take four consecutive
 // chunk positions, so each SIMD holds one contiguous quarter of every row's
@@ -265,6 +269,7 @@ __device__ __forceinline__ bool sub_p1(const SubCtx<Q> &c, int r, const SubChunk
     const int sv = sub_stage_issue(c, r + 1);  // row r+1's indices, committed below
     if (rc.cnt > 0) {
         const int nj = sub_nj(c, rc);
+        const int njt = c.live ? nj : 0;  // the |t| <= 1e-10 vote: frame-less lanes abstain
         const uint16_t *lc = sub_lcols(c, r, rc);
         const uint32_t eoff = sub_eoff(c, rc);
         // iteration 0 / a fresh streaming frame: M = L (E_old is loaded anyway
@@ -309,7 +314,7 @@ __device__ __forceinline__ bool sub_p1(const SubCtx<Q> &c, int r, const SubChunk
                     const int i = g0 + q;
                     if (i < K) {
                         const double tv = th[q];
-                        tiny |= i < nj && !(fabs(tv) > kTiny);
+                        tiny |= i < njt && !(fabs(tv) > kTiny);
                         // slots past this lane's piece: 1.0, an exact no-op in the chain product
                         t[i] = i < nj ? tv : 1.0;
                     }
@@ -455,19 +460,20 @@ __device__ __forceinline__ void sub_p3_body(SubCtx<Q> &c, int r, double (&t)[Sub
         // every quotient of the wavefront is below 2^-27, where that is exact
         // (spa_math.h kAtanhIdent; the common case on long rows at low SNR)
         bool big = false;
-        if (div_nr_ok(P)) {
+        const double lim = c.live ? kAtanhIdent : INFINITY;  // frame-less lanes do not vote
+        if (div_nr_ok(c.live ? P : 1.0)) {
 #pragma unroll
             for (int i = 0; i < K; ++i)
                 if (i < rc.CS) {
                     t[i] = div_nr(P, t[i]);
-                    big |= !(fabs(t[i]) < kAtanhIdent);
+                    big |= !(fabs(t[i]) < lim);
                 }
         } else {
 #pragma unroll
             for (int i = 0; i < K; ++i)
                 if (i < rc.CS) {
                     t[i] = P / t[i];
-                    big |= !(fabs(t[i]) < kAtanhIdent);
+                    big |= !(fabs(t[i]) < lim);
                 }
         }
         if (__ballot(big) == 0ull) {

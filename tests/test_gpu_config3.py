@@ -36,8 +36,11 @@ def _want(H, u, llr):
 
 
 @pytest.mark.parametrize("snr,step", [(1.0, 3), (1.0, 7), (2.0, 5), (3.0, 6)])
-def test_bench_step_counters_equal_oracle(gpu_available, snr, step):
-    """One bench step's call (one SNR point per call, snr_point 0), 64 frames."""
+def test_bench_step_counters_equal_oracle(gpu_available, snr, step, monkeypatch):
+    """One bench step's call (one SNR point per call, snr_point 0), 64 frames.
+    The bench's 512-tile chunks run the sub-tile decoder; so does this 1-tile
+    call once the small-batch column-parallel path is off (LDPC_SMALL_COLS=0)."""
+    monkeypatch.setenv("LDPC_SMALL_COLS", "0")
     H = hstd_for(CODE)
     B = 64
     frame0 = STEP * step + 1000 * step

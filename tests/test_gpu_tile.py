@@ -18,6 +18,14 @@ from test_gpu_parity import _random_llr
 pytestmark = pytest.mark.gpu
 
 
+@pytest.fixture(autouse=True)
+def _tile_path_at_any_size(monkeypatch):
+    """These tests exercise the tile kernels on small batches: keep the
+    small-batch column-parallel path (LDPC_SMALL_COLS, test_gpu_smallcols.py)
+    out of the way."""
+    monkeypatch.setenv("LDPC_SMALL_COLS", "0")
+
+
 def _decoder(code, frames):
     from ldpc_amd.device import Decoder, Graph
     return Decoder(Graph.cached(hstd_for(code)), frames)
