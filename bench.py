@@ -14,7 +14,10 @@ on the device.  With N GPUs (one process per GPU, launched by
 torch.distributed.run) every rank decodes its own disjoint frame range and the
 counters are summed with ONE all-reduce over RCCL (weak scaling).  After the
 timed region, one step each at --extra-snr points (default 2.0 and 3.0 dB) is
-timed and reported under "snr_points", and a few steps of the physical mode
+timed and reported under "snr_points" (scope "step"), then --point-snr (default
+3.0 dB) as ONE whole config-3 point of 262,144 frames per GPU streamed in one
+run (scope "point": the streaming tail is paid once per point, as main.py pays
+it), and a few steps of the physical mode
 (the north-star's absolute cw/s target, NOT the
 reference's arithmetic) under "physical".
 
@@ -69,6 +72,11 @@ def parse():
     ap.add_argument("--snr", type=float, default=1.0, help="reference SNR axis (dB), speed=1")
     ap.add_argument("--extra-snr", default="2.0,3.0",
                     help="comma-separated SNR points timed for one step each after the headline ('' = none)")
+    ap.add_argument("--point-snr", default="3.0",
+                    help="comma-separated SNR points streamed as ONE whole point of --point-frames frames per GPU "
+                         "(config 3's per-SNR batch; the streaming tail is paid once per point, as in main.py's "
+                         "per-point loop) and reported under 'snr_points' with scope 'point' ('' = none)")
+    ap.add_argument("--point-frames", type=int, default=262144, help="frames per GPU of a whole --point-snr point")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU-baseline sample budget (0 = skip)")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = every usable host core (usable_cores())")
     ap.add_argument("--mode", choices=("parity", "physical"), default="parity",
@@ -493,9 +501,38 @@ def main():
         barrier(dist, local)
         dt = max_over_ranks(dist, time.perf_counter() - t1, local)
         f = int(c[0, 0])
-        snr_points.append({"snr_db": x, "value": f / dt, "unit": "codewords/s", "info_bits_per_s": f * k / dt,
+        snr_points.append({"snr_db": x, "scope": "step", "value": f / dt, "unit": "codewords/s",
+                           "info_bits_per_s": f * k / dt,
                            "ms": dt * 1e3, "frames": f, "schedule": extra_sched, "slots": extra_slots,
                            "avg_iters": int(c[0, 6]) / max(f, 1),
+                           "fer": int(c[0, 1]) / max(f, 1), "ber": int(c[0, 2]) / (k * max(f, 1))})
+    # whole SNR points: config 3's 262,144 frames of one point streamed through
+    # the same slots in ONE mc_run (frame indices after every step above), so
+    # the point's tail -- its last failing frames finishing their 50 passes on
+    # few tiles -- is paid once per point, as main.py pays it once per point
+    whole = [v for v in args.point_snr.split(",") if v.strip()] if pgraph is None else []
+    if whole and extra_slots is None:
+        dec.close()
+        extra_slots = max(64, (B // 4) // 64 * 64)
+        dec = Decoder(graph, extra_slots)
+        dec.mc_run(SEED, [1.0 / math.sqrt(2.0 * 10.0 ** (float(whole[0]) * 0.1))], 64, 1 << 40, args.iters,
+                   static=False, split=args.split)
+    base = (args.warmup + args.steps + len(extra)) * world * B
+    for i, x in enumerate(whole):
+        x = float(x)
+        sg = 1.0 / math.sqrt(2.0 * 1.0 * (10.0 ** (x * 0.1)))
+        PF = args.point_frames
+        barrier(dist, local)
+        t1 = time.perf_counter()
+        c = dec.mc_run(SEED, [sg], PF, base + (i * world + rank) * PF, args.iters, static=False, split=args.split)
+        c = allreduce_counters(dist, c, local)
+        barrier(dist, local)
+        dt = max_over_ranks(dist, time.perf_counter() - t1, local)
+        f = int(c[0, 0])
+        assert f == PF * world, (f, PF, world)
+        snr_points.append({"snr_db": x, "scope": "point", "value": f / dt, "unit": "codewords/s",
+                           "info_bits_per_s": f * k / dt, "ms": dt * 1e3, "frames": f, "schedule": "stream",
+                           "slots": extra_slots, "avg_iters": int(c[0, 6]) / max(f, 1),
                            "fer": int(c[0, 1]) / max(f, 1), "ber": int(c[0, 2]) / (k * max(f, 1))})
 
     physical = None

@@ -14,8 +14,8 @@
 //                   fp64 ch (parity decoder, LDS physical decoder, export) or as
 //                   the tile physical decoder's fp32 Lambda = L = -llr
 // Every kernel has >= ntiles x (n/128 or m/128) wavefronts, so even a small
-// chunk fills the chip (the per-lane generator gen_lane in spa_kernels.hip
-// remains for the streaming refill, where single lanes are regenerated).
+// chunk fills the chip (the streaming refill, where single slots are
+// regenerated, uses frame_source.h's gen_slots: the same draws).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>

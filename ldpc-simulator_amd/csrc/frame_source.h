@@ -60,55 +60,72 @@ __device__ __forceinline__ unsigned long long wave_sum(unsigned long long v) {
     return v;
 }
 
-// ------------------------------------------------ per-lane frame generation
-// (streaming refill; whole chunks use frame_kernels.hip).  u bits live in LDS
-// ([kw][64], each lane reads only its own column, so no barrier is needed).
-// Frame F of SNR point `snr_point` into lane `lane` of `tile`: info bits (ubits
-// and the lane's LDS column `ul`), channel LLRs ch[tile][j][lane].  With
-// `set_L`, also L = ch (a streaming refill: the next CN then forms M = L - 0).
-__device__ inline void gen_lane(const DevGraph &g, const DevState &st, int tile, int lane, int64_t F, uint64_t seed,
-                         int snr_point, double sigma, const uint32_t *__restrict__ apack, uint32_t *ul, bool valid,
-                         bool set_L) {
+// ------------------------------------------------ cooperative slot refill
+// Streaming refill by the WHOLE workgroup, with generate_kernel's draws
+// (frame_kernels.hip: the same frames bit for bit): slot f (0..F-1, tile lane lane0 + f) takes frame
+// gidx[f], or nothing when gidx[f] < 0.  ustage: LDS [kw][F] words, zero on
+// return (a refilled slot's words are written before they are read; the
+// caller puts a barrier after).  Thread
+// t = worker * F + f: first the info words as (Philox block, slot) tasks,
+// then column pairs worker, worker + nworkers, ... of every refilled slot --
+// all wavefronts share the n/2 noise draws and m parity rows of a frame that
+// one wavefront generated alone before (a 2304-bit frame: ~40 % of a pass of
+// the streaming sub-tile decoder at 3 dB, where most slots refill every pass).
+// Every thread of the block calls it (it holds two barriers).
+template <int F>
+__device__ inline void gen_slots(const DevGraph &g, const DevState &st, int tile, int lane0, const long long *gidx,
+                                 uint32_t *ustage, uint64_t seed, int snr_point, double sigma) {
     const int kw = (g.k + 31) >> 5;
-    // info bits: data_buffer.py:23 / generator.py:7-9 (random.randint(0,1) per bit)
-    for (int blk = 0; blk * 4 < kw; ++blk) {
+    const int nthr = blockDim.x;
+    // info bits: data_buffer.py:23 / generator.py:7-9
+    for (int t = threadIdx.x; t < ((kw + 3) >> 2) * F; t += nthr) {
+        const int f = t % F, blk = t / F;
+        const long long Fi = gidx[f];
+        if (Fi < 0) continue;
         uint32_t c[4];
-        info_block(seed, F, snr_point, blk, c);
+        info_block(seed, Fi, snr_point, blk, c);
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
             const int w = blk * 4 + q;
             if (w >= kw) break;
             uint32_t v = c[q];
             if (w == kw - 1 && (g.k & 31)) v &= (1u << (g.k & 31)) - 1u;
-            ul[w * kTile + lane] = v;
-            st.ubits[((size_t)tile * kw + w) * kTile + lane] = v;
+            ustage[w * F + f] = v;
+            st.ubits[((size_t)tile * kw + w) * kTile + lane0 + f] = v;
         }
     }
-    // codeword [u, A.u mod 2] + BPSK + AWGN (channel.py:49,68-80)
-    const double s2 = sigma * sigma;
-    double *Ct = st.ch + (size_t)tile * g.n * kTile + lane;
-    double *Lt = st.L + (size_t)tile * g.n * kTile + lane;
-    for (int jb = 0; jb < g.n; jb += 2) {
-        double gz[2];
-        noise_pair(seed, F, snr_point, jb >> 1, gz);
+    __syncthreads();
+    // codeword [u, A.u mod 2] + BPSK + AWGN (channel.py:49,68-80), L = ch
+    const int f = threadIdx.x % F, worker = threadIdx.x / F, nwork = nthr / F;
+    const long long Fi = gidx[f];
+    if (Fi >= 0) {
+        const double s2 = sigma * sigma;
+        double *Ct = st.ch + (size_t)tile * g.n * kTile + lane0 + f;
+        double *Lt = st.L + (size_t)tile * g.n * kTile + lane0 + f;
+        for (int b = worker; 2 * b < g.n; b += nwork) {
+            double gz[2];
+            noise_pair(seed, Fi, snr_point, b, gz);
 #pragma unroll
-        for (int q = 0; q < 2; ++q) {
-            const int j = jb + q;
-            if (j >= g.n) break;
-            uint32_t bit;
-            if (j < g.k) {
-                bit = (ul[(j >> 5) * kTile + lane] >> (j & 31)) & 1u;
-            } else {  // parity bit of row j-k = parity(A_row & u), A bit-packed (uniform loads)
-                const uint32_t *ar = apack + (size_t)(j - g.k) * kw;
-                uint32_t acc = 0u;
-                for (int w = 0; w < kw; ++w) acc ^= ar[w] & ul[w * kTile + lane];
-                bit = (uint32_t)__popc(acc) & 1u;
+            for (int q = 0; q < 2; ++q) {
+                const int j = 2 * b + q;
+                if (j >= g.n) break;
+                uint32_t bit;
+                if (j < g.k) {
+                    bit = (ustage[(j >> 5) * F + f] >> (j & 31)) & 1u;
+                } else {  // parity(A_row & u), A bit-packed
+                    const uint32_t *ar = g.a_packed + (size_t)(j - g.k) * kw;
+                    uint32_t acc = 0u;
+                    for (int w = 0; w < kw; ++w) acc ^= ar[w] & ustage[w * F + f];
+                    bit = (uint32_t)__popc(acc) & 1u;
+                }
+                const double llr = channel_llr(bit, gz[q], s2);
+                Ct[(size_t)j * kTile] = llr;
+                Lt[(size_t)j * kTile] = llr;
             }
-            const double llr = valid ? channel_llr(bit, gz[q], s2) : 0.0;
-            Ct[j * kTile] = llr;
-            if (set_L) Lt[j * kTile] = llr;
         }
     }
+    __syncthreads();
+    for (int i = threadIdx.x; i < kw * F; i += nthr) ustage[i] = 0u;
 }
 
 }  // namespace ldpc

@@ -114,10 +114,6 @@ __global__ __launch_bounds__(256, LDPC_CN_WAVES) void cn_kernel(DevGraph g, DevS
                                                                 int it_parity, const int *__restrict__ col_idx,
                                                                 const int *__restrict__ row_ptr, AtanhCoef ac) {
     __shared__ MathLds mlds;
-    fill_math_lds(mlds);
-    __syncthreads();
-    const LdsTanh ttab{mlds.tanh};
-    const LdsLog ltab{mlds.log};
     const int lane = threadIdx.x & 63;
     const int wave = uniform(threadIdx.x >> 6);
     // XCD-aware mapping: blocks b and b+8 share an XCD (round-robin dispatch),
@@ -127,8 +123,14 @@ __global__ __launch_bounds__(256, LDPC_CN_WAVES) void cn_kernel(DevGraph g, DevS
     const int slot = b >> 3;
     const int tile = (slot / blocks_per_tile) * 8 + (b & 7);
     const int row = (slot % blocks_per_tile) * kCnRowsPerBlock + wave;
-    if (tile >= st.ntiles || row >= g.m) return;
-    if (!st.tile_active[tile]) return;
+    // block-uniform: a block of a finished (or padding) tile leaves before
+    // staging the math tables
+    if (tile >= st.ntiles || !st.tile_active[tile]) return;
+    fill_math_lds(mlds);
+    __syncthreads();
+    const LdsTanh ttab{mlds.tanh};
+    const LdsLog ltab{mlds.log};
+    if (row >= g.m) return;
     const int beg = row_ptr[row], end = row_ptr[row + 1];
     if (beg == end) return;  // spa_decoder.py:115-122
 
@@ -222,17 +224,17 @@ __global__ __launch_bounds__(64 * W, WPS) void cn_row_kernel(DevGraph g, DevStat
                                                              const int *__restrict__ row_ptr, AtanhCoef ac) {
     __shared__ MathLds mlds;
     __shared__ double chain[kTile];  // running product handed from wavefront to wavefront
-    fill_math_lds(mlds);
-    __syncthreads();
-    const LdsTanh ttab{mlds.tanh};
-    const LdsLog ltab{mlds.log};
     const int lane = threadIdx.x & 63;
     const int wave = uniform(threadIdx.x >> 6);
     const int b = blockIdx.x;  // XCD-aware: every row of a tile on the tile's XCD
     const int slot = b >> 3;
     const int tile = (slot / g.m) * 8 + (b & 7);
     const int row = slot % g.m;
-    if (tile >= st.ntiles || !st.tile_active[tile]) return;  // block-uniform
+    if (tile >= st.ntiles || !st.tile_active[tile]) return;  // block-uniform, before the table staging
+    fill_math_lds(mlds);
+    __syncthreads();
+    const LdsTanh ttab{mlds.tanh};
+    const LdsLog ltab{mlds.log};
     const int beg = row_ptr[row], end = row_ptr[row + 1];
     const int deg = end - beg;
     if (deg == 0) return;  // spa_decoder.py:115-122
@@ -733,34 +735,50 @@ __global__ void export_msgs_kernel(DevGraph g, DevState st, double *out) {
 
 // Streaming refill (Monte-Carlo path): every lane flagged by vn_kernel (or, at
 // the start, every lane) takes the next frame index from one device counter
-// (wave-aggregated atomicAdd) and generates it in place; with no frame left the
-// lane goes idle.  Lanes of one tile therefore decode different frames at
+// (wave-aggregated atomicAdd; wave 0 of the tile's block) and the block's 8
+// wavefronts generate the new frames in place (gen_slots); with no frame left
+// the lane goes idle.  Lanes of one tile therefore decode different frames at
 // different iterations -- each lane's state depends on its own frame only.
-__global__ __launch_bounds__(64) void refill_kernel(DevGraph g, DevState st, uint64_t seed, int snr_point,
-                                                    double sigma, int64_t frame0, int64_t total,
-                                                    unsigned long long *next, const uint32_t *__restrict__ apack) {
-    extern __shared__ uint32_t ul[];
+constexpr int kRefillThreads = 512;  // 8 wavefronts share a tile's frame generation (gen_slots)
+__global__ __launch_bounds__(kRefillThreads) void refill_kernel(DevGraph g, DevState st, uint64_t seed,
+                                                                int snr_point, double sigma, int64_t frame0,
+                                                                int64_t total, unsigned long long *next) {
+    extern __shared__ uint32_t ul[];  // [kw][64] u-bit stage
+    __shared__ long long gidx[kTile];
+    __shared__ int gen;
     const int tile = blockIdx.x;
-    const int lane = threadIdx.x;
+    const int lane = threadIdx.x & 63;
     const int f = tile * kTile + lane;
-    const bool need = st.refill[f] != 0;
-    const unsigned long long want = __ballot(need);
-    if (want == 0ull) return;
-    const unsigned long long below = lane ? (want & (~0ull >> (64 - lane))) : 0ull;
-    unsigned long long base = 0ull;
-    if (lane == __ffsll((long long)want) - 1) base = atomicAdd(next, (unsigned long long)__popcll(want));
-    base = __shfl(base, __ffsll((long long)want) - 1);
-    const int64_t idx = (int64_t)(base + (unsigned long long)__popcll(below));
-    const bool have = need && idx < total;
-    if (have) gen_lane(g, st, tile, lane, frame0 + idx, seed, snr_point, sigma, apack, ul, true, true);
-    if (need) {
-        st.refill[f] = 0;
-        st.done[f] = have ? 0 : 1;
-        st.fresh[f] = have ? 1 : 0;
-        st.iters[f] = 0;
+    if (threadIdx.x < kTile) {  // wave 0: the lanes to refill take the next indices
+        const bool need = st.refill[f] != 0;
+        const unsigned long long want = __ballot(need);
+        bool have = false;
+        long long gi = -1;
+        if (want != 0ull) {
+            const unsigned long long below = lane ? (want & (~0ull >> (64 - lane))) : 0ull;
+            unsigned long long base = 0ull;
+            if (lane == __ffsll((long long)want) - 1) base = atomicAdd(next, (unsigned long long)__popcll(want));
+            base = __shfl(base, __ffsll((long long)want) - 1);
+            const int64_t idx = (int64_t)(base + (unsigned long long)__popcll(below));
+            have = need && idx < total;
+            if (have) gi = (long long)(frame0 + idx);
+            if (need) {
+                st.refill[f] = 0;
+                st.done[f] = have ? 0 : 1;
+                st.fresh[f] = have ? 1 : 0;
+                st.iters[f] = 0;
+            }
+        }
+        gidx[lane] = gi;
+        const unsigned long long busy = __ballot(st.done[f] == 0);
+        const unsigned long long took = __ballot(have);  // (a ballot of the whole wavefront)
+        if (lane == 0) {
+            if (want != 0ull) st.tile_active[tile] = busy != 0ull ? 1 : 0;
+            gen = took != 0ull ? 1 : 0;
+        }
     }
-    const unsigned long long busy = __ballot(st.done[f] == 0);
-    if (lane == 0) st.tile_active[tile] = busy != 0ull ? 1 : 0;
+    __syncthreads();
+    if (gen) gen_slots<kTile>(g, st, tile, 0, gidx, ul, seed, snr_point, sigma);
 }
 
 __global__ void export_frames_kernel(DevGraph g, DevState st, uint8_t *u_out, double *llr_out) {
@@ -846,12 +864,14 @@ bool use_cn_row(const DevGraph &g) {
 // (16 B instead of 24 B per edge, one tanh per edge instead of two); in the
 // few-tile streaming tail, where one 16-wavefront workgroup per CU is all
 // that fits, 1.5 % slower (profiles/r2aw_cn_row16).  LDPC_CN_ROW16 (read per
-// call): 0 = never, 1 = at any tile count, unset = from 64 tiles.
+// call): 0 = never, 1 = at any tile count, N > 1 = from N tiles, unset = from
+// 64 tiles.
 constexpr int kRow16W = 16, kRow16K = 40;
 bool use_cn_row16(const DevGraph &g, int ntiles) {
     if (use_cn_row(g) || g.max_row_deg > kRow16W * kRow16K) return false;
     const char *e = getenv("LDPC_CN_ROW16");
-    return e ? atoi(e) != 0 : ntiles >= 64;
+    const int from = e ? atoi(e) : 64;
+    return from != 0 && ntiles >= from;
 }
 
 template <bool kFirst, bool kStream>
@@ -946,7 +966,7 @@ hipError_t launch_stream_init(const DevGraph &, const DevState &st, hipStream_t 
 hipError_t launch_refill(const DevGraph &g, const DevState &st, uint64_t seed, int snr_point, double sigma,
                          int64_t frame0, int64_t total, unsigned long long *next, hipStream_t s) {
     const size_t lds = (size_t)((g.k + 31) >> 5) * kTile * sizeof(uint32_t);
-    refill_kernel<<<st.ntiles, kTile, lds, s>>>(g, st, seed, snr_point, sigma, frame0, total, next, g.a_packed);
+    refill_kernel<<<st.ntiles, kRefillThreads, lds, s>>>(g, st, seed, snr_point, sigma, frame0, total, next);
     return hipGetLastError();
 }
 

@@ -245,7 +245,7 @@ __device__ __forceinline__ void t8_prefetch(const T8Ctx<K> &c, int r, T8Pre<K> &
 #pragma unroll
         for (int i = 0; i < K; ++i) p.eo[i] = c.first ? 0.0 : t8_ld<kNT>(c.rE, t8_es(c, eoff, i));
     }
-    if (c.wave == c.idwave && rc.deg > 0) {  // identity edge (a fresh streaming frame has L = ch: gen_lane)
+    if (c.wave == c.idwave && rc.deg > 0) {  // identity edge (a fresh streaming frame has L = ch: gen_slots)
         p.lid = t8_ld(c.first ? c.rC : c.rL, ((uint32_t)(c.k + r) << 9) + c.lo8);
         p.eid = c.first ? 0.0 : t8_ld<kNT>(c.rE, ((uint32_t)(rc.beg + rc.deg - 1) << 6) + c.eo8);
     }

@@ -466,16 +466,16 @@ __global__ __launch_bounds__(64 * kTW, 1) void tile_kernel(DevGraph g, DevState 
 // iteration: after each pass a lane whose frame stopped adds that frame's
 // counters (count_kernel's definitions, main.py:130-138) and takes the next
 // frame index from one device counter; the frame is generated in place
-// (gen_lane: ch and L = ch, so the next pass forms M = L - 0, its iteration
+// (gen_slots: ch and L = ch, so the next pass forms M = L - 0, its iteration
 // 0).  Every frame is decoded exactly as in the static schedule (the lane's
 // state depends on its own frame only), so the counters are identical.  The
 // workgroup exits once the supply is exhausted and its lanes have drained.
 // wave 0 of the streaming kernel: lanes with `want` take the next frame
-// indices (one wave-aggregated atomicAdd) and generate them (inlined: as a
-// real call the register saves around it cost 10x).
-__device__ __forceinline__ void tile_refill(const DevGraph &g, const DevState &st, int tile, int lane, bool want,
-                                         uint64_t seed, int snr_point, double sigma, int64_t frame0, int64_t total,
-                                         unsigned long long *next, uint32_t *ul, int *livel, int *freshl, int *itl) {
+// indices (one wave-aggregated atomicAdd) into gidx; the whole workgroup then
+// generates them (frame_source.h gen_slots).  -> some lane took a frame.
+__device__ __forceinline__ bool tile_refill(int lane, bool want, int64_t frame0, int64_t total,
+                                           unsigned long long *next, long long *gidx, int *livel, int *freshl,
+                                           int *itl) {
     const unsigned long long w = __ballot(want);
     const int first = __ffsll((long long)w) - 1;
     unsigned long long base = 0ull;
@@ -484,12 +484,13 @@ __device__ __forceinline__ void tile_refill(const DevGraph &g, const DevState &s
     const unsigned long long below = lane ? (w & (~0ull >> (64 - lane))) : 0ull;
     const int64_t idx = (int64_t)(base + (unsigned long long)__popcll(below));
     const bool have = want && idx < total;
-    if (have) gen_lane(g, st, tile, lane, frame0 + idx, seed, snr_point, sigma, g.a_packed, ul, true, true);
+    gidx[lane] = have ? (long long)(frame0 + idx) : -1ll;
     if (want) {
         livel[lane] = have ? 1 : 0;
         freshl[lane] = have ? 1 : 0;
         itl[lane] = 0;
     }
+    return __ballot(have) != 0ull;
 }
 
 __global__ __launch_bounds__(64 * kTW, 1) void tile_stream_kernel(DevGraph g, DevState st, int max_iter, int nllr,
@@ -510,6 +511,8 @@ __global__ __launch_bounds__(64 * kTW, 1) void tile_stream_kernel(DevGraph g, De
     int *livel = cntl + kTile;
     int *flags = (int *)(lds + ly.flags);
     __shared__ int itl[kTile], freshl[kTile];
+    __shared__ long long gidx[kTile];  // refill: lane's new frame index (< 0: none)
+    __shared__ int nref;               // refill: some lane took a frame this pass
     const int kw = (g.k + 31) >> 5, mw = (g.m + 31) >> 5;
     const int tile = blockIdx.x;
     if (tile >= st.ntiles) return;  // block-uniform
@@ -554,20 +557,28 @@ __global__ __launch_bounds__(64 * kTW, 1) void tile_stream_kernel(DevGraph g, De
     const uint32_t *Ut = st.ubits + (size_t)tile * kw * kTile + lane;
 
     for (int pass = 0;; ++pass) {
-        // refill: lanes without a frame take the next indices and generate
-        // them (wave 0, one frame per lane; u bits staged in zb)
+        // refill: lanes without a frame take the next indices (wave 0), and
+        // the whole workgroup generates them (u bits staged in zb, which still
+        // holds the last pass's z^1 bits: gen_slots writes a refilled lane's
+        // words before reading them and clears zb; without a refill it is
+        // cleared here)
         if (wave == 0) {
-            if (__ballot(want) != 0ull)
-                tile_refill(g, st, tile, lane, want, seed, snr_point, sigma, frame0, total, next, zb, livel, freshl,
-                            itl);
+            bool gen = false;
+            if (__ballot(want) != 0ull) gen = tile_refill(lane, want, frame0, total, next, gidx, livel, freshl, itl);
             want = false;
             const unsigned long long any = __ballot(livel[lane] != 0);
-            if (lane == 0) flags[2 * kTR + 1] = any != 0ull ? 1 : 0;
+            if (lane == 0) {
+                flags[2 * kTR + 1] = any != 0ull ? 1 : 0;
+                nref = gen ? 1 : 0;
+            }
         }
-        __syncthreads();  // the generator staged u bits in zb: clear only after it
-        for (int i = threadIdx.x; i < kw * kTile; i += blockDim.x) zb[i] = 0u;
         __syncthreads();
         if (!flags[2 * kTR + 1]) break;  // supply exhausted, every lane drained
+        if (nref)
+            gen_slots<kTile>(g, st, tile, 0, gidx, zb, seed, snr_point, sigma);
+        else
+            for (int i = threadIdx.x; i < kw * kTile; i += blockDim.x) zb[i] = 0u;
+        __syncthreads();
 
         c.live = livel[lane] != 0;
         c.fresh = freshl[lane] != 0;
@@ -652,7 +663,7 @@ __global__ __launch_bounds__(64 * kTW, 1) void tile_stream_kernel(DevGraph g, De
             cntl[lane] = 0;
         }
         for (int i = threadIdx.x; i < mw * kTile; i += blockDim.x) ib[i] = 0u;
-        // zb is cleared (and reused as the u-bit stage) at the top of the loop
+        // zb is reused as the u-bit stage and cleared at the top of the loop
     }
 }
 
@@ -701,8 +712,9 @@ bool use_tile_stream(const DevGraph &g) {
     const char *e = getenv("LDPC_TILE_STREAM");
     if (e && atoi(e) == 0) return false;
     const size_t lds = tile64_lds_bytes(g);
-    // + the kernel's static per-lane state (itl, freshl: 2 x 64 ints)
-    if (lds) return lds + 2 * kTile * sizeof(int) <= kTileLdsMax;
+    // + the kernel's static per-lane state (itl, freshl: 2 x 64 ints; gidx: 64
+    // frame indices; the refill flag)
+    if (lds) return lds + 2 * kTile * sizeof(int) + kTile * sizeof(long long) + 16 <= kTileLdsMax;
     if (g.ef == 8) return false;  // tile8.hip: static launches; streaming runs the split loop
     return sub16(g);
 }

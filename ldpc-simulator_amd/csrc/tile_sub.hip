@@ -97,7 +97,7 @@ constexpr int kStaticBF = SUB_STATIC_BF;
 #endif
 constexpr int kStreamBF = SUB_STREAM_BF;
 // the branch-free hop (Q = 4) multiplies all K slots: P1 must pad them (bit 0)
-static_assert((kStaticBF & 1) && (kStreamBF & 1), "the branch-free hop needs the branch-free P1");
+static_assert(((kStaticBF & kStreamBF) & 1) != 0, "the branch-free hop needs the branch-free P1");
 // Logical wavefront (chunk position in a row) of hardware wavefront hw: the
 // four wavefronts of one SIMD (hw = s, s+4, s+8, s+12) take four consecutive
 // chunk positions, so each SIMD holds one contiguous quarter of every row's
@@ -772,7 +772,7 @@ __global__ __launch_bounds__(64 * kSW, 1) void tile_sub_kernel(DevGraph g, DevSt
 // at 16 frames per workgroup): every frame slot f is at its own iteration;
 // after each pass a slot whose frame stopped adds that frame's counters
 // (count_kernel's definitions, main.py:130-138) and takes the next frame
-// index from one device counter; the frame is generated in place (gen_lane:
+// index from one device counter; the frame is generated in place (gen_slots:
 // ch and L = ch, so its next pass forms M = L - 0, its iteration 0).  Each
 // frame decodes exactly as in the static schedule, so the counters are
 // identical.  A workgroup exits once the supply is out and its slots drained.
@@ -784,6 +784,8 @@ __global__ __launch_bounds__(64 * kSW, 1) void tile_sub_stream_kernel(
     constexpr int F = SubCfg<Q>::F, K = SubCfg<Q>::K;
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     __shared__ int itl[F], freshl[F];
+    __shared__ long long gidx[F];  // refill: slot f's new frame index (< 0: none)
+    __shared__ int nref;           // refill: some slot took a frame this pass
     const SubLayout ly = sub_layout(g.k, g.m, F);
     double *S = (double *)(lds + ly.S);
     MathLds &mlds = *(MathLds *)(lds + ly.math);
@@ -850,11 +852,10 @@ __global__ __launch_bounds__(64 * kSW, 1) void tile_sub_stream_kernel(
     const int m = g.m;
     const int nthr = kSW * Q;
     const int me = wave * Q + j;
-    uint32_t *ul = st.ubits + (size_t)tile * kw * kTile;  // u-bit stage: the slots' own ubits words
     const uint32_t *Ut = st.ubits + (size_t)tile * kw * kTile + lane64;
 
     for (int pass = 0;; ++pass) {
-        if (wave == 0) {  // refill: slots without a frame take the next indices and generate them
+        if (wave == 0) {  // refill: slots without a frame take the next indices (generated below)
             // hand-off: once the supply is out and at most `handoff` frames
             // are still running anywhere, stop here and leave them to the
             // column-parallel tail (ldpc_api.cpp mc_stream_point): a running
@@ -868,6 +869,7 @@ __global__ __launch_bounds__(64 * kSW, 1) void tile_sub_stream_kernel(
             stop = uniform(stop);
             if (stop) want = false;
             const unsigned long long w = __ballot(want);
+            bool have = false;
             if (w != 0ull) {
                 const int first = __ffsll((long long)w) - 1;
                 unsigned long long base = 0ull;
@@ -875,14 +877,15 @@ __global__ __launch_bounds__(64 * kSW, 1) void tile_sub_stream_kernel(
                 base = __shfl(base, first);
                 const unsigned long long below = lane ? (w & (~0ull >> (64 - lane))) : 0ull;
                 const int64_t idx = (int64_t)(base + (unsigned long long)__popcll(below));
-                const bool have = want && idx < total;
-                if (have) gen_lane(g, st, tile, lane64, frame0 + idx, seed, snr_point, sigma, g.a_packed, ul, true, true);
+                have = want && idx < total;
+                if (slot_lane) gidx[f] = have ? (long long)(frame0 + idx) : -1ll;
                 if (want) {
                     livel[f] = have ? 1 : 0;
                     freshl[f] = have ? 1 : 0;
                     itl[f] = 0;
                 }
             }
+            const bool gen = __ballot(have) != 0ull;
             want = false;
             const unsigned long long any = __ballot(slot_lane && livel[f] != 0);
             const bool go = any != 0ull && !stop;
@@ -893,10 +896,16 @@ __global__ __launch_bounds__(64 * kSW, 1) void tile_sub_stream_kernel(
                 st.fresh[fr] = freshl[f];
                 st.refill[fr] = 0;
             }
-            if (lane == 0) flags[2 * kSR + 1] = go ? 1 : 0;
+            if (lane == 0) {
+                flags[2 * kSR + 1] = go ? 1 : 0;
+                nref = go && gen ? 1 : 0;
+            }
         }
         __syncthreads();
         if (!flags[2 * kSR + 1]) break;  // supply exhausted, every slot drained
+        // the new frames, generated by the whole workgroup (u bits staged in
+        // zb, which is zero here and again after)
+        if (nref) gen_slots<F>(g, st, tile, sub * F, gidx, zb, seed, snr_point, sigma);
         c.live = livel[f] != 0;
         c.fresh = freshl[f] != 0;
         c.ep0 = sub_epoch0(pass, m);
@@ -1003,8 +1012,9 @@ hipError_t launch_tile_sub_stream(const DevGraph &g, const DevState &st, int max
                                   int snr_point, double sigma, int64_t frame0, int64_t total,
                                   unsigned long long *next, unsigned long long *ctr, int64_t handoff, hipStream_t s) {
     const size_t lds = sub_lds_bytes_q<4>(g);
-    // the 16-frame form only (+ 2 x 16 ints of static LDS per-slot state)
-    if (!lds || !g.a_packed || !st.ubits || st.ntiles > st.nslots || lds + 2 * 16 * sizeof(int) > kSubLdsMax)
+    // the 16-frame form only (+ static LDS: 2 x 16 ints, 16 frame indices, the refill flag)
+    if (!lds || !g.a_packed || !st.ubits || st.ntiles > st.nslots ||
+        lds + 2 * 16 * sizeof(int) + 16 * sizeof(long long) + 16 > kSubLdsMax)
         return hipErrorInvalidValue;
     tile_sub_stream_kernel<4><<<st.ntiles * 4, 64 * kSW, lds, s>>>(g, st, max_iter, nllr ? 1 : 0, g.col_idx, g.row_ptr,
                                                                    kAtanhCoef, seed, snr_point, sigma, frame0, total,

@@ -6,7 +6,7 @@ d = json.loads([ln for ln in open(sys.argv[1]) if ln.startswith("{")][-1])
 r = d.get("roofline") or {}
 out = {"value": round(d["value"] or 0), "n_gpus": d.get("n_gpus"), "kernel": r.get("kernel"),
        "frac": round(r.get("frac", 0), 4), "avg_launch_ms": round(r.get("avg_launch_ms", 0), 1),
-       "snr_points": [(p["snr_db"], round(p["value"])) for p in d.get("snr_points", [])]}
+       "snr_points": [(p["snr_db"], p.get("scope", "step"), round(p["value"])) for p in d.get("snr_points", [])]}
 ph = d.get("physical")
 if ph:
     out["physical"] = (round(ph["value"]), round(ph.get("roofline", {}).get("frac", 0), 3), round(ph["avg_iters"], 2))
