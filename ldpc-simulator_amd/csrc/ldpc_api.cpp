@@ -73,6 +73,7 @@ struct ldpc_decoder {
     int *cpairs = nullptr;  // streaming tail compaction plan (1 + 2 cap ints), on first use
     uint32_t *tzb = nullptr;  // streaming tail VN: z^1 bits [cap_tiles][ceil(n/32)][64], zero between uses
     int *tcnt = nullptr;      // streaming tail VN: normalized-LLR counts [cap_tiles*64], zero between uses
+    int *tbad = nullptr;      // few-frame decode path: row-parity flags [cap_tiles*64], zero between uses
     DevState st{};
     // profiling (ldpc_profile_*)
     bool prof = false;
@@ -273,16 +274,31 @@ bool small_batch_cols(const DevGraph &G, int ntiles) {
     return !ldpc::use_tile(G) || ldpc::sub_frames(G) == 16 || G.ef == 8;
 }
 
+// Few frames: the lanes of a wavefront take a row's / column's edges instead
+// of frames (edge_kernels.hip), so a pass's loads are all in flight at once --
+// main.py's one-frame decode() calls: one wimax_2304_0.5 frame at T=50 in
+// 5.1 ms instead of 102 ms, 8 frames in 20 ms (a frame costs ~2 ms more;
+// profiles/r3g_edge).  LDPC_EDGE_FRAMES (read per call): the batch size up to
+// which it applies (default 32, below the frame-per-lane path's ~100 ms;
+// 0 = never).
+bool small_batch_edge(const DevGraph &G, int count) {
+    const char *e = getenv("LDPC_EDGE_FRAMES");
+    const int lim = e ? atoi(e) : 32;
+    return count <= lim && G.max_row_deg <= ldpc::edge_max_deg() && G.max_col_deg <= ldpc::edge_max_deg();
+}
+
 // the column-parallel VN's per-tile buffers (zero between passes)
 int ensure_tail_bufs(ldpc_decoder *d, hipStream_t s) {
     const DevGraph &G = d->g->dg;
     const int cap = d->cap_tiles * kTile;
     const size_t nzb = (size_t)d->cap_tiles * ((G.n + 31) / 32) * kTile;
-    if (!d->tzb && (dev_alloc(&d->tzb, nzb) || dev_alloc(&d->tcnt, (size_t)cap))) return LDPC_ENOMEM;
+    if (!d->tzb && (dev_alloc(&d->tzb, nzb) || dev_alloc(&d->tcnt, (size_t)cap) || dev_alloc(&d->tbad, (size_t)cap)))
+        return LDPC_ENOMEM;
     // tail_exit_kernel leaves them zero, but a call that stopped early (an
     // error return) may not have: cleared per call, never trusted
     if (hipMemsetAsync(d->tzb, 0, nzb * sizeof(uint32_t), s) != hipSuccess ||
-        hipMemsetAsync(d->tcnt, 0, (size_t)cap * sizeof(int), s) != hipSuccess)
+        hipMemsetAsync(d->tcnt, 0, (size_t)cap * sizeof(int), s) != hipSuccess ||
+        hipMemsetAsync(d->tbad, 0, (size_t)cap * sizeof(int), s) != hipSuccess)
         return ldpc_fail(LDPC_EDEVICE, "tail buffers: memset failed");
     return LDPC_OK;
 }
@@ -296,6 +312,7 @@ hipError_t run_iterations(ldpc_decoder *d, const DevGraph &G, const DevState &st
     hipError_t e = hipSuccess;
     DevState st = st_in;
     const bool cols = small_batch_cols(G, st.ntiles) && ensure_tail_bufs(d, s) == LDPC_OK;
+    const bool edge = cols && small_batch_edge(G, st.count);
     if (!split && !cols && ldpc::use_tile(G) && st.ntiles <= st.nslots)  // one launch: every tile to its own exit
         return timed(d, LDPC_K_TILE, s, [&] { return ldpc::launch_tile(G, st, max_iter, nllr, s); });
     // cn_rare_kernel clears the OTHER parity's count for the next CN; the one
@@ -313,10 +330,17 @@ hipError_t run_iterations(ldpc_decoder *d, const DevGraph &G, const DevState &st
         st.active_count = d->pactive;
     }
     for (int it = 0; it < max_iter && e == hipSuccess; ++it) {
-        e = timed(d, LDPC_K_CN, s, [&] { return ldpc::launch_cn(G, st, it, s); });
-        if (e == hipSuccess) e = ldpc::launch_cn_rare(G, st, it, s);
+        if (edge) {  // the rare rows are handled inside cn_edge_kernel
+            e = timed(d, LDPC_K_CN, s, [&] { return ldpc::launch_cn_edge(G, st, it, s); });
+        } else {
+            e = timed(d, LDPC_K_CN, s, [&] { return ldpc::launch_cn(G, st, it, s); });
+            if (e == hipSuccess) e = ldpc::launch_cn_rare(G, st, it, s);
+        }
         if (e == hipSuccess)
             e = timed(d, LDPC_K_VN, s, [&] {
+                if (edge)
+                    return ldpc::launch_vn_edge_decode(G, st, it, it + 1 == max_iter, nllr, d->tzb, d->tcnt, d->tbad,
+                                                       s);
                 return cols ? ldpc::launch_vn_cols_decode(G, st, it, it + 1 == max_iter, nllr, d->tzb, d->tcnt, s)
                             : ldpc::launch_vn(G, st, it, max_iter, nllr, s);
             });
@@ -584,6 +608,7 @@ int ldpc_decoder_destroy(ldpc_decoder *d) {
     (void)hipFree(d->cpairs);
     (void)hipFree(d->tzb);
     (void)hipFree(d->tcnt);
+    (void)hipFree(d->tbad);
     (void)hipFree(d->L);
     (void)hipFree(d->ch);
     (void)hipFree(d->ints);

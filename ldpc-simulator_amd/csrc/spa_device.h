@@ -129,6 +129,18 @@ hipError_t launch_vn_tail(const DevGraph &g, const DevState &st, int max_iter, b
                           unsigned long long *ctr, hipStream_t s);
 hipError_t launch_vn_cols_decode(const DevGraph &g, const DevState &st, int it, bool last, bool nllr, uint32_t *zb,
                                  int *cnt, hipStream_t s);
+// tail_exit_kernel's decode exits; gbad (null: the kernel forms the syndrome
+// itself) holds the per-frame row-parity flags of syn_kernel, cleared after use
+hipError_t launch_tail_exit_decode(const DevGraph &g, const DevState &st, int it, bool last, bool nllr, uint32_t *zb,
+                                   int *cnt, int *gbad, hipStream_t s);
+// few-frame decode path (edge_kernels.hip): lanes over a row's / column's
+// edges, frame after frame; bit-identical to launch_cn + launch_cn_rare and
+// launch_vn_cols_decode.  Rows and columns of up to edge_max_deg() edges;
+// gbad [cap_tiles*64] int, zero on entry (left zero)
+int edge_max_deg();
+hipError_t launch_cn_edge(const DevGraph &g, const DevState &st, int it, hipStream_t s);
+hipError_t launch_vn_edge_decode(const DevGraph &g, const DevState &st, int it, bool last, bool nllr, uint32_t *zb,
+                                 int *cnt, int *gbad, hipStream_t s);
 hipError_t launch_refill(const DevGraph &g, const DevState &st, uint64_t seed, int snr_point, double sigma,
                          int64_t frame0, int64_t total, unsigned long long *next, hipStream_t s);
 // streaming tail: move the frames running in tiles >= nt into finished slots

@@ -564,10 +564,12 @@ constexpr int kTailKw = 64;  // (z^1)_A words held per lane: k <= 2048
 // `last` whether it is the final one, and the exits are vn_kernel<.., false>'s
 // (conv / status / iters, the normalized-LLR history, the host poll's count);
 // otherwise `last` is max_iter and the exits are the streaming ones.
+// gbad (decode only, may be null): the row parities were already OR-ed into
+// gbad[frame] by syn_kernel (edge_kernels.hip); read and cleared here.
 template <bool kDecode>
 __global__ __launch_bounds__(64 * kTailWaves) void tail_exit_kernel(DevGraph g, DevState st, int it, int last,
                                                                      int nllr, uint32_t *zb, int *cnt,
-                                                                     unsigned long long *ctr) {
+                                                                     unsigned long long *ctr, int *gbad) {
     __shared__ int bad[kTile];
     const int tile = blockIdx.x;
     if (!st.tile_active[tile]) return;  // block-uniform
@@ -576,26 +578,28 @@ __global__ __launch_bounds__(64 * kTailWaves) void tail_exit_kernel(DevGraph g, 
     const int f = tile * kTile + lane;
     const int kw = (g.k + 31) >> 5, nw = (g.n + 31) >> 5;
     uint32_t *zt = zb + (size_t)tile * nw * kTile + lane;
-    if (threadIdx.x < kTile) bad[threadIdx.x] = 0;
+    if (threadIdx.x < kTile) bad[threadIdx.x] = (kDecode && gbad) ? gbad[f] : 0;
     __syncthreads();
     uint32_t za[kTailKw];
+    if (!(kDecode && gbad)) {
 #pragma unroll
-    for (int w = 0; w < kTailKw; ++w) {
-        uint32_t v = w < kw ? zt[w * kTile] : 0u;
-        if (w == kw - 1 && (g.k & 31)) v &= (1u << (g.k & 31)) - 1u;  // A columns only
-        za[w] = v;
-    }
-    uint32_t acc = 0u;
-    for (int r = wave; r < g.m; r += kTailWaves) {
-        const uint32_t *ar = g.a_packed + (size_t)r * kw;
-        const int q = g.k + r;  // identity column of row r
-        uint32_t par = zt[(q >> 5) * kTile] >> (q & 31);
+        for (int w = 0; w < kTailKw; ++w) {
+            uint32_t v = w < kw ? zt[w * kTile] : 0u;
+            if (w == kw - 1 && (g.k & 31)) v &= (1u << (g.k & 31)) - 1u;  // A columns only
+            za[w] = v;
+        }
+        uint32_t acc = 0u;
+        for (int r = wave; r < g.m; r += kTailWaves) {
+            const uint32_t *ar = g.a_packed + (size_t)r * kw;
+            const int q = g.k + r;  // identity column of row r
+            uint32_t par = zt[(q >> 5) * kTile] >> (q & 31);
 #pragma unroll
-        for (int w = 0; w < kTailKw; ++w)
-            if (w < kw) par += __builtin_popcount(ar[w] & za[w]);
-        acc |= par & 1u;
+            for (int w = 0; w < kTailKw; ++w)
+                if (w < kw) par += __builtin_popcount(ar[w] & za[w]);
+            acc |= par & 1u;
+        }
+        if (acc) atomicOr(&bad[lane], 1);
     }
-    if (acc) atomicOr(&bad[lane], 1);
     __syncthreads();
     if (kDecode && wave == 0) {  // vn_kernel<.., false>'s exits
         const bool live = st.done[f] == 0;
@@ -626,6 +630,7 @@ __global__ __launch_bounds__(64 * kTailWaves) void tail_exit_kernel(DevGraph g, 
             if (any && st.active_count) atomicAdd(&st.active_count[it], 1);  // host poll: 0 -> all stopped
         }
         cnt[f] = 0;
+        if (gbad) gbad[f] = 0;
     }
     if (!kDecode && wave == 0) {  // vn_kernel<false, true>'s exits and counters
         const bool live = st.done[f] == 0;
@@ -942,7 +947,8 @@ hipError_t launch_vn_tail(const DevGraph &g, const DevState &st, int max_iter, b
     if (!g.a_packed || !st.ubits || ((g.k + 31) >> 5) > kTailKw) return hipErrorInvalidValue;
     vn_cols_kernel<<<dim3((unsigned)((g.n + 3) / 4), (unsigned)st.ntiles), 256, 0, s>>>(g, st, nllr ? 1 : 0, zb, cnt,
                                                                                       0);
-    tail_exit_kernel<false><<<st.ntiles, 64 * kTailWaves, 0, s>>>(g, st, 0, max_iter, nllr ? 1 : 0, zb, cnt, ctr);
+    tail_exit_kernel<false><<<st.ntiles, 64 * kTailWaves, 0, s>>>(g, st, 0, max_iter, nllr ? 1 : 0, zb, cnt, ctr,
+                                                                  nullptr);
     return hipGetLastError();
 }
 
@@ -952,8 +958,13 @@ hipError_t launch_vn_cols_decode(const DevGraph &g, const DevState &st, int it, 
     if (!g.a_packed || ((g.k + 31) >> 5) > kTailKw) return hipErrorInvalidValue;
     vn_cols_kernel<<<dim3((unsigned)((g.n + 3) / 4), (unsigned)st.ntiles), 256, 0, s>>>(g, st, nllr ? 1 : 0, zb, cnt,
                                                                                       it == 0 ? 1 : 0);
+    return launch_tail_exit_decode(g, st, it, last, nllr, zb, cnt, nullptr, s);
+}
+
+hipError_t launch_tail_exit_decode(const DevGraph &g, const DevState &st, int it, bool last, bool nllr, uint32_t *zb,
+                                   int *cnt, int *gbad, hipStream_t s) {
     tail_exit_kernel<true><<<st.ntiles, 64 * kTailWaves, 0, s>>>(g, st, it, last ? 1 : 0, nllr ? 1 : 0, zb, cnt,
-                                                                 nullptr);
+                                                                 nullptr, gbad);
     return hipGetLastError();
 }
 
