@@ -279,11 +279,15 @@ bool small_batch_cols(const DevGraph &G, int ntiles) {
 // main.py's one-frame decode() calls: one wimax_2304_0.5 frame at T=50 in
 // 5.1 ms instead of 102 ms, 8 frames in 20 ms (a frame costs ~2 ms more;
 // profiles/r3g_edge).  LDPC_EDGE_FRAMES (read per call): the batch size up to
-// which it applies (default 32, below the frame-per-lane path's ~100 ms;
-// 0 = never).
+// which it applies (default 32 for the 2304 codes, below the frame-per-lane
+// path's ~100 ms; 4 for the codes of the 64-frame tile_kernel, whose one
+// launch takes 7.9 ms for wimax_576_0.5 against 2.9 ms + ~1.1 ms per frame;
+// 0 = never; LDPC_SMALL_COLS=0, which keeps every small-batch path away, too).
 bool small_batch_edge(const DevGraph &G, int count) {
+    const char *c = getenv("LDPC_SMALL_COLS");
+    if (c && atoi(c) == 0) return false;
     const char *e = getenv("LDPC_EDGE_FRAMES");
-    const int lim = e ? atoi(e) : 32;
+    const int lim = e ? atoi(e) : (ldpc::tile64_lds_bytes(G) > 0 ? 4 : 32);
     return count <= lim && G.max_row_deg <= ldpc::edge_max_deg() && G.max_col_deg <= ldpc::edge_max_deg();
 }
 
@@ -311,8 +315,11 @@ hipError_t run_iterations(ldpc_decoder *d, const DevGraph &G, const DevState &st
                           hipStream_t s, bool poll, bool split) {
     hipError_t e = hipSuccess;
     DevState st = st_in;
-    const bool cols = small_batch_cols(G, st.ntiles) && ensure_tail_bufs(d, s) == LDPC_OK;
-    const bool edge = cols && small_batch_edge(G, st.count);
+    // the edge path applies to every [A | I] code with k <= 2048 (the 64-frame
+    // tile codes too: one wimax_576_0.5 frame, profiles/r3g_edge)
+    const bool edge = G.a_packed && ((G.k + 31) >> 5) <= 64 && tail_vn_enabled() && small_batch_edge(G, st.count) &&
+                      ensure_tail_bufs(d, s) == LDPC_OK;
+    const bool cols = edge || (small_batch_cols(G, st.ntiles) && ensure_tail_bufs(d, s) == LDPC_OK);
     if (!split && !cols && ldpc::use_tile(G) && st.ntiles <= st.nslots)  // one launch: every tile to its own exit
         return timed(d, LDPC_K_TILE, s, [&] { return ldpc::launch_tile(G, st, max_iter, nllr, s); });
     // cn_rare_kernel clears the OTHER parity's count for the next CN; the one
