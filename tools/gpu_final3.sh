@@ -1,0 +1,12 @@
+#!/bin/bash
+# round-3 final evidence: -m gpu suite, smoke, default bench, rocprof trace + FETCH/WRITE PMC of the headline.
+set -o pipefail
+export TMPDIR=/tmp
+T=${TAG:-final3}
+O=gpurun_out/$T; mkdir -p $O
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > $O/gpu_tests.log 2>&1 || { echo TESTS_FAILED; grep -E "FAIL|Error" $O/gpu_tests.log | head -20; tail -30 $O/gpu_tests.log; exit 1; }
+tail -1 $O/gpu_tests.log
+timeout -k 10 120 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 && tail -1 $O/smoke.log || exit 1
+timeout -k 10 400 python -u bench.py > $O/bench_default.json 2> $O/bench_default.err || { tail -20 $O/bench_default.err; exit 1; }
+python tools/bench_summary.py $O/bench_default.json
+bash tools/profile_tile.sh ${T}_prof && echo PROF_OK

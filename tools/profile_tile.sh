@@ -8,7 +8,7 @@
 # usage: tools/profile_tile.sh TAG ; outputs under gpurun_out/TAG
 set -e
 TAG=${1:-prof_tile}
-ARGS="--steps 2 --warmup 1 --cpu-seconds 0 --extra-snr= --phys-steps 0"
+ARGS="--steps 2 --warmup 1 --cpu-seconds 0 --extra-snr= --point-snr= --phys-steps 0"
 export TMPDIR=/tmp
 OUT=gpurun_out/$TAG
 mkdir -p $OUT
