@@ -87,7 +87,8 @@ def parse():
     ap.add_argument("--phys-steps", type=int, default=4,
                     help="parity mode: timed physical-mode steps reported under 'physical' after the "
                          "headline (0 = none); not the reference's arithmetic (SURVEY 8 f4)")
-    ap.add_argument("--phys-frames", type=int, default=65536, help="frames per physical-mode step")
+    ap.add_argument("--phys-frames", type=int, default=262144,
+                    help="frames per physical-mode step (config 3's batch; 65,536 measured 2.7 % slower: host syncs)")
     ap.add_argument("--stub", action="store_true",
                     help="launcher rehearsal without a GPU: every rank only joins a gloo group and "
                          "counts the ranks (tests/test_bench_launch.py); also LDPC_BENCH_STUB=1")
