@@ -63,9 +63,23 @@ __device__ __forceinline__ void frame_load(const PhysArgs &a, int f, float *E, f
     for (int e = tid; e < g.nnz; e += nt) E[e] = 0.0f;
 }
 
+// Monte-Carlo counters of the frames one workgroup decodes (thread 0's
+// registers), added to the device counters once, when the workgroup is done:
+// one atomic per counter per frame on the same 7 addresses serialised every
+// frame of a launch in L2.
+struct FrameCounts {
+    unsigned long long v[7] = {0, 0, 0, 0, 0, 0, 0};
+    __device__ __forceinline__ void flush(unsigned long long *ctr) const {
+        if (!ctr) return;
+#pragma unroll
+        for (int i = 0; i < 7; ++i)
+            if (v[i]) atomicAdd(&ctr[i], v[i]);
+    }
+};
+
 // Outputs and Monte-Carlo counters of frame f (conv = -1: not converged).
 __device__ __forceinline__ void frame_finish(const PhysArgs &a, int f, int conv, const float *L, int *s_err,
-                                             int tid, int nt) {
+                                             int tid, int nt, FrameCounts &fc) {
     const DevGraph &g = a.g;
     const int iters = conv >= 0 ? conv + 1 : a.max_iter;
     for (int j = tid; j < g.n; j += nt) {
@@ -92,15 +106,15 @@ __device__ __forceinline__ void frame_finish(const PhysArgs &a, int f, int conv,
         }
         __syncthreads();
         if (tid == 0) {
-            atomicAdd(&a.ctr[0], 1ull);
+            fc.v[0] += 1ull;
             if (conv < 0) {
-                atomicAdd(&a.ctr[1], 1ull);
-                atomicAdd(&a.ctr[2], (unsigned long long)*s_err);
+                fc.v[1] += 1ull;
+                fc.v[2] += (unsigned long long)*s_err;
             } else {
-                atomicAdd(&a.ctr[3], (unsigned long long)conv);
-                atomicAdd(&a.ctr[4], 1ull);
+                fc.v[3] += (unsigned long long)conv;
+                fc.v[4] += 1ull;
             }
-            atomicAdd(&a.ctr[6], (unsigned long long)iters);
+            fc.v[6] += (unsigned long long)iters;
         }
     }
     __syncthreads();  // LDS reused by the next frame
@@ -113,6 +127,7 @@ __global__ __launch_bounds__(256) void phys_kernel(PhysArgs a) {
     float *L = E + ((g.nnz + 3) & ~3);  // [n]
     float *Lam = L + ((g.n + 3) & ~3);  // [n]
     __shared__ int s_err;
+    FrameCounts fc;
     const int tid = threadIdx.x, nt = blockDim.x;
     for (int f = blockIdx.x; f < a.count; f += gridDim.x) {
         frame_load(a, f, E, L, Lam, tid, nt);
@@ -155,8 +170,9 @@ __global__ __launch_bounds__(256) void phys_kernel(PhysArgs a) {
                 break;
             }
         }
-        frame_finish(a, f, conv, L, &s_err, tid, nt);
+        frame_finish(a, f, conv, L, &s_err, tid, nt, fc);
     }
+    if (tid == 0) fc.flush(a.ctr);
 }
 
 // The same decoder with every thread's rows and columns fixed for the whole
@@ -173,6 +189,7 @@ __global__ __launch_bounds__(NT, WPS) void phys_reg_kernel(PhysArgs a) {
     float *L = E + ((g.nnz + 3) & ~3);
     float *Lam = L + ((g.n + 3) & ~3);
     __shared__ int s_err;
+    FrameCounts fc;
     const int tid = threadIdx.x;
     int rbeg[RPT], rdeg[RPT];
     uint32_t rc[RPT][RDEG / 2];
@@ -263,8 +280,9 @@ __global__ __launch_bounds__(NT, WPS) void phys_reg_kernel(PhysArgs a) {
                 break;
             }
         }
-        frame_finish(a, f, conv, L, &s_err, tid, NT);
+        frame_finish(a, f, conv, L, &s_err, tid, NT, fc);
     }
+    if (tid == 0) fc.flush(a.ctr);
 }
 
 }  // namespace
