@@ -89,6 +89,8 @@ def parse():
                          "headline (0 = none); not the reference's arithmetic (SURVEY 8 f4)")
     ap.add_argument("--phys-frames", type=int, default=262144,
                     help="frames per physical-mode step (config 3's batch; 65,536 measured 2.7 % slower: host syncs)")
+    ap.add_argument("--dropin-calls", type=int, default=20,
+                    help="parity mode: one-frame decode() calls timed under 'dropin' (main.py's call pattern; 0 = none)")
     ap.add_argument("--stub", action="store_true",
                     help="launcher rehearsal without a GPU: every rank only joins a gloo group and "
                          "counts the ranks (tests/test_bench_launch.py); also LDPC_BENCH_STUB=1")
@@ -393,6 +395,33 @@ def physical_extra(args, edd, graph, local, world, rank, dist, k):
     return out
 
 
+def dropin_extra(args, graph, n):
+    """main.py's call pattern through the drop-in SPA_Decoder: decode() of ONE
+    frame per call (python_ldpc_app/main.py:124,312; 64 slots, as
+    ldpc_amd.SPA_Decoder), which runs the few-frame edge path.  Synthetic
+    frames: the all-zero codeword through the reference channel model (bit 0 ->
+    -1, noise std sigma^2, LLR 2y/sigma^2: channel.py:49,68-80), host numpy RNG;
+    each call uploads the frame and reads z / conv / status back, as decode()
+    does.  Timed after everything else."""
+    from ldpc_amd.device import Decoder
+    d = Decoder(graph, 64)
+    sg = 1.0 / math.sqrt(2.0 * 1.0 * (10.0 ** (args.snr * 0.1)))
+    s2 = sg * sg
+    rng = np.random.default_rng(SEED)
+    llr = 2.0 * (-1.0 + s2 * rng.standard_normal((args.dropin_calls + 1, n))) / s2
+    d.decode(llr[:1], args.iters)  # warm-up (workspace, first launches)
+    iters = 0
+    t0 = time.perf_counter()
+    for i in range(1, args.dropin_calls + 1):
+        iters += int(d.decode(llr[i:i + 1], args.iters).iters[0])
+    dt = time.perf_counter() - t0
+    d.close()
+    return {"what": "drop-in decode(): one frame per call, main.py's loop (few-frame edge path)",
+            "frames_per_call": 1, "calls": args.dropin_calls, "ms_per_call": dt / args.dropin_calls * 1e3,
+            "value": args.dropin_calls / dt, "unit": "codewords/s", "avg_iters": iters / args.dropin_calls,
+            "max_iter": args.iters, "snr_db": args.snr, "data": "all-zero codeword, reference channel model"}
+
+
 def main():
     args = parse()
     launched = "WORLD_SIZE" in os.environ
@@ -540,6 +569,7 @@ def main():
     if args.phys_steps > 0 and pgraph is None and not ira_code:
         dec.close()
         physical = physical_extra(args, edd, graph, local, world, rank, dist, k)
+    dropin = dropin_extra(args, graph, n) if args.dropin_calls > 0 and pgraph is None else None
 
     frames_total = int(totals[0, 0])
     assert frames_total == B * world * args.steps, (frames_total, B, world, args.steps)
@@ -613,6 +643,8 @@ def main():
         out["snr_points"] = snr_points
     if physical is not None:
         out["physical"] = physical
+    if dropin is not None:
+        out["dropin"] = dropin
     if not tile_launches and pgraph is None and cn_launches:
         # separate CN / VN launches: the roofline is the WHOLE decode, one "launch" = one
         # CN + one VN sweep over the resident slots; traffic = PMC bytes of the same pair

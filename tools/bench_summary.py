@@ -10,6 +10,9 @@ out = {"value": round(d["value"] or 0), "n_gpus": d.get("n_gpus"), "kernel": r.g
 ph = d.get("physical")
 if ph:
     out["physical"] = (round(ph["value"]), round(ph.get("roofline", {}).get("frac", 0), 3), round(ph["avg_iters"], 2))
+di = d.get("dropin")
+if di:
+    out["dropin_ms"] = round(di["ms_per_call"], 2)
 cb = d.get("cpu_baseline")
 if cb:
     out["cpu"] = (round(cb["value"], 2), cb["cores"])

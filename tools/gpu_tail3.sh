@@ -3,7 +3,7 @@
 set -o pipefail
 export TMPDIR=/tmp
 O=gpurun_out/${TAG:-tail3}; mkdir -p $O
-S="--snr 3.0 --schedule stream --chunk 8192 --frames 32768 --steps 1 --warmup 1 --cpu-seconds 0 --extra-snr= --phys-steps 0"
+S="--snr 3.0 --schedule stream --chunk 8192 --frames 32768 --steps 1 --warmup 1 --cpu-seconds 0 --extra-snr= --point-snr= --phys-steps 0"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/trace -o run -- python3 bench.py $S > $O/b.log 2>&1 || { tail $O/b.log; exit 1; }
 python3 - <<'PY'
 import csv,glob
