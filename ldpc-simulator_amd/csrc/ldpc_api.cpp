@@ -68,6 +68,8 @@ struct ldpc_decoder {
     uint32_t *pbits = nullptr;
     int *pactive = nullptr;  // [pactive_cap] tiles still running after VN(it)
     int pactive_cap = 0;
+    double *hist = nullptr;  // decode's normalized-LLR history [cap][hist_cap], kept between calls
+    int hist_cap = 0;        // (main.py's one-frame calls ask for it every time: no hipMalloc per call)
     unsigned long long *counters = nullptr;  // [counters_cap] + 1 frame-index counter (streaming)
     int counters_cap = 0;
     int *cpairs = nullptr;  // streaming tail compaction plan (1 + 2 cap ints), on first use
@@ -616,6 +618,7 @@ int ldpc_decoder_destroy(ldpc_decoder *d) {
     (void)hipFree(d->tzb);
     (void)hipFree(d->tcnt);
     (void)hipFree(d->tbad);
+    (void)hipFree(d->hist);
     (void)hipFree(d->L);
     (void)hipFree(d->ch);
     (void)hipFree(d->ints);
@@ -670,16 +673,19 @@ int ldpc_decode_f64(ldpc_decoder *d, int32_t batch, const double *llr, int32_t m
     std::vector<double> h_dbl;
     int rc = LDPC_OK;
     if (nllr_hist) {
-        if ((rc = dev_alloc(&d_hist, (size_t)cap * max_iter))) return rc;
+        if (d->hist_cap < max_iter) {  // grow-only, reused by later calls
+            (void)hipFree(d->hist);
+            d->hist = nullptr;
+            d->hist_cap = 0;
+            if ((rc = dev_alloc(&d->hist, (size_t)cap * max_iter))) return rc;
+            d->hist_cap = max_iter;
+        }
+        d_hist = d->hist;
     }
     if (msg_out) {
-        if ((rc = dev_alloc(&d_msgs, (size_t)cap * G.nnz))) {
-            (void)hipFree(d_hist);
-            return rc;
-        }
+        if ((rc = dev_alloc(&d_msgs, (size_t)cap * G.nnz))) return rc;
     }
     auto fail_dev = [&](hipError_t e, const char *what) {
-        (void)hipFree(d_hist);
         (void)hipFree(d_msgs);
         return ldpc_fail(LDPC_EDEVICE, "ldpc_decode_f64: %s: %s", what, hipGetErrorString(e));
     };
@@ -765,7 +771,6 @@ int ldpc_decode_f64(ldpc_decoder *d, int32_t batch, const double *llr, int32_t m
     if (d_hist || d_msgs) {
         if ((e = hipStreamSynchronize(s))) return fail_dev(e, "sync");
     }
-    (void)hipFree(d_hist);
     (void)hipFree(d_msgs);
     if ((e = hipGetLastError())) return ldpc_fail(LDPC_EDEVICE, "ldpc_decode_f64: %s", hipGetErrorString(e));
     return LDPC_OK;

@@ -17,7 +17,7 @@ rng = np.random.default_rng(1)
 Bs = [int(b) for b in os.environ.get("BS", "1,64,256,1024").split(",")]
 for B in Bs:
     dec = Decoder(g, max(B, 64))
-    llr = rng.normal(2.0, 2.0, size=(B, n))
+    llr = rng.normal(float(os.environ.get("MEAN", "2.0")), 2.0, size=(B, n))
     ref = None
     for var in sys.argv[1:]:
         keys = []
