@@ -24,7 +24,8 @@
 //                   normalized-LLR count (:210-228): vn_cols_kernel's outputs
 //   syn_kernel      row parities popcount(A_r & (z^1)_A) + (z^1)_{k+r}
 //                   (:191-204) over many workgroups (lane = frame), OR-ed
-//                   into a per-frame flag that tail_exit_kernel then reads
+//                   into a per-frame flag that tail_exit_kernel then reads;
+//                   syn_row_kernel (<= 4 frames): the same with lane = row
 // Bit-identical to the split path (tests/test_gpu_edge.py).  Used by
 // ldpc_decode_f64 for batches of at most LDPC_EDGE_FRAMES frames (ldpc_api.cpp).
 #include <hip/hip_runtime.h>
@@ -241,6 +242,39 @@ __global__ __launch_bounds__(256) void syn_kernel(DevGraph g, DevState st, const
     if (acc) atomicOr(&bad[f], 1);
 }
 
+// The same row parities with lane = ROW (64 rows per wavefront), frame after
+// frame: a few frames leave most lanes of syn_kernel idle (one frame: 1 of 64)
+// and its 8-row chains set its time (~22 us); here a lane's A row is loaded
+// once into registers and each frame's (z^1)_A words are wave-uniform.
+constexpr int kSynRowFrames = 4;  // syn_row_kernel up to this many frames (one frame: 4.94 vs 5.30 ms; 8: 20.7 vs 20.0)
+__global__ __launch_bounds__(256) void syn_row_kernel(DevGraph g, DevState st, const uint32_t *zb, int *bad) {
+    const int tile = blockIdx.y;
+    if (!st.tile_active[tile]) return;
+    const int lane = threadIdx.x & 63;
+    const int r = ((int)blockIdx.x * 4 + uniform(threadIdx.x >> 6)) * 64 + lane;  // this lane's row
+    const int kw = (g.k + 31) >> 5, nw = (g.n + 31) >> 5;
+    const bool row_ok = r < g.m;
+    uint32_t ar[kSynKw];
+#pragma unroll
+    for (int w = 0; w < kSynKw; ++w) {
+        uint32_t v = (row_ok && w < kw) ? g.a_packed[(size_t)r * kw + w] : 0u;
+        if (w == kw - 1 && (g.k & 31)) v &= (1u << (g.k & 31)) - 1u;  // A columns only
+        ar[w] = v;
+    }
+    const int q = g.k + (row_ok ? r : 0);  // identity column of row r
+    unsigned long long live = __ballot(st.done[tile * kTile + lane] == 0);  // (lane as a frame index here)
+    while (live != 0ull) {
+        const int f = __ffsll((long long)live) - 1;  // uniform
+        live &= live - 1ull;
+        const uint32_t *zt = zb + (size_t)tile * nw * kTile + f;
+        uint32_t par = zt[(q >> 5) * kTile] >> (q & 31);
+#pragma unroll
+        for (int w = 0; w < kSynKw; ++w)
+            if (w < kw) par += __builtin_popcount(ar[w] & zt[w * kTile]);
+        if (__ballot(row_ok && (par & 1u)) != 0ull && lane == 0) atomicOr(&bad[tile * kTile + f], 1);
+    }
+}
+
 }  // namespace
 
 int edge_max_deg() { return 64 * kEdgeKE; }
@@ -260,8 +294,13 @@ hipError_t launch_vn_edge_decode(const DevGraph &g, const DevState &st, int it, 
     if (!g.a_packed || g.max_col_deg > 64 * kEdgeKE || ((g.k + 31) >> 5) > kSynKw) return hipErrorInvalidValue;
     vn_edge_kernel<<<dim3((unsigned)((g.n + 3) / 4), (unsigned)st.ntiles), 256, 0, s>>>(g, st, nllr ? 1 : 0, zb, cnt,
                                                                                       it == 0 ? 1 : 0);
-    const int waves = (g.m + kSynRows - 1) / kSynRows;
-    syn_kernel<<<dim3((unsigned)((waves + 3) / 4), (unsigned)st.ntiles), 256, 0, s>>>(g, st, zb, bad);
+    if (st.count <= kSynRowFrames) {
+        const int waves = (g.m + 63) / 64;
+        syn_row_kernel<<<dim3((unsigned)((waves + 3) / 4), (unsigned)st.ntiles), 256, 0, s>>>(g, st, zb, bad);
+    } else {
+        const int waves = (g.m + kSynRows - 1) / kSynRows;
+        syn_kernel<<<dim3((unsigned)((waves + 3) / 4), (unsigned)st.ntiles), 256, 0, s>>>(g, st, zb, bad);
+    }
     return launch_tail_exit_decode(g, st, it, last, nllr, zb, cnt, bad, s);
 }
 
