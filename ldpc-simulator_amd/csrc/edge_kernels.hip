@@ -50,7 +50,10 @@ __device__ __forceinline__ double readlane_d(double x, int l) {
     return dfrom(((uint64_t)hi << 32) | lo);
 }
 
-template <bool kFirst>
+// KE: edges per lane, fixed per graph (ceil(max_row_deg / 64) rounded up to
+// 4, 8, 12 or 16) so every slot loop is static: a row-dependent count made the
+// compiler keep a guard per slot and spill SGPRs to VGPR lanes.
+template <bool kFirst, int KE>
 __global__ __launch_bounds__(256) void cn_edge_kernel(DevGraph g, DevState st, AtanhCoef ac) {
     __shared__ MathLds mlds;
     const int tile = blockIdx.y;
@@ -64,36 +67,30 @@ __global__ __launch_bounds__(256) void cn_edge_kernel(DevGraph g, DevState st, A
     if (row >= g.m) return;
     const int beg = g.row_ptr[row], deg = g.row_ptr[row + 1] - beg;
     if (deg == 0) return;  // spa_decoder.py:115-122
-    const int KE = (deg + 63) >> 6;          // uniform; <= kEdgeKE (host checks max_row_deg)
-    const int nlanes = (deg + KE - 1) / KE;  // lanes holding edges
+    const int nlanes = (deg + KE - 1) / KE;  // lanes holding edges (deg <= 64 KE: host check)
     const int p0 = lane * KE;
     const int nl = max(0, min(deg - p0, KE));  // this lane's edges; slots past them repeat the last edge
-    int col[kEdgeKE];
+    int col[KE];
 #pragma unroll
-    for (int i = 0; i < kEdgeKE; ++i)
-        if (i < KE) col[i] = g.col_idx[beg + min(p0 + i, deg - 1)];
+    for (int i = 0; i < KE; ++i) col[i] = g.col_idx[beg + min(p0 + i, deg - 1)];
     unsigned long long live = __ballot(st.done[tile * kTile + lane] == 0);
     while (live != 0ull) {
         const int f = __ffsll((long long)live) - 1;  // uniform
         live &= live - 1ull;
         double *Ef = st.E + e_base(g, tile, f);
         const double *Lf = (kFirst ? st.ch : st.L) + (size_t)tile * g.n * kTile + f;
-        double t[kEdgeKE];
+        double t[KE];
 #pragma unroll
-        for (int i = 0; i < kEdgeKE; ++i) {
-            if (i < KE) {
-                double M = Lf[(size_t)col[i] * kTile];
-                if (!kFirst) M = M - Ef[(size_t)(beg + min(p0 + i, deg - 1)) * g.ef];  // :260-268
-                t[i] = M;
-            }
+        for (int i = 0; i < KE; ++i) {
+            double M = Lf[(size_t)col[i] * kTile];
+            if (!kFirst) M = M - Ef[(size_t)(beg + min(p0 + i, deg - 1)) * g.ef];  // :260-268
+            t[i] = M;
         }
         uint32_t tiny = 0u;  // this lane's slots with |t| <= 1e-10
 #pragma unroll
-        for (int i = 0; i < kEdgeKE; ++i) {
-            if (i < KE) {
-                t[i] = cn_tanh(t[i], ttab);
-                if (i < nl && !(fabs(t[i]) > kTiny)) tiny |= 1u << i;
-            }
+        for (int i = 0; i < KE; ++i) {
+            t[i] = cn_tanh(t[i], ttab);
+            if (i < nl && !(fabs(t[i]) > kTiny)) tiny |= 1u << i;
         }
         // P = t0 * t1 * ... left to right (1.0 * t0 == t0 exactly)
         double P = 1.0;
@@ -101,31 +98,27 @@ __global__ __launch_bounds__(256) void cn_edge_kernel(DevGraph g, DevState st, A
             double x = P;
             if (lane == l) {
 #pragma unroll
-                for (int i = 0; i < kEdgeKE; ++i)
+                for (int i = 0; i < KE; ++i)
                     if (i < nl) x = x * t[i];
             }
             P = readlane_d(x, l);
         }
-        double En[kEdgeKE];
+        double En[KE];
         if (__ballot(tiny != 0u) == 0ull) {
             // q = P/t (div_nr: the IEEE quotient when P is not tiny, cn_common.h);
             // E_new = 2 atanh(clip(q)), or 2q where every quotient of the
             // wavefront is below 2^-27 (exact: spa_math.h kAtanhIdent)
             const bool nr = div_nr_ok(P);
 #pragma unroll
-            for (int i = 0; i < kEdgeKE; ++i) {
-                if (i < KE) {
-                    const double q = nr ? div_nr(P, t[i]) : P / t[i];
-                    En[i] = __ballot(!(fabs(q) < kAtanhIdent)) == 0ull ? 2.0 * q
-                                                                        : 2.0 * atanh_f(clip_cl(q), ltab, ac);
-                }
+            for (int i = 0; i < KE; ++i) {
+                const double q = nr ? div_nr(P, t[i]) : P / t[i];
+                En[i] = __ballot(!(fabs(q) < kAtanhIdent)) == 0ull ? 2.0 * q : 2.0 * atanh_f(clip_cl(q), ltab, ac);
             }
         } else {
             // rare (cn_rare_kernel's arithmetic): q = P/t, and for an edge with
             // |t| <= 1e-10 the in-order product of the others (:164)
 #pragma unroll
-            for (int i = 0; i < kEdgeKE; ++i)
-                if (i < KE) En[i] = 2.0 * atanh_f(clip_cl(P / t[i]), ltab, ac);
+            for (int i = 0; i < KE; ++i) En[i] = 2.0 * atanh_f(clip_cl(P / t[i]), ltab, ac);
             unsigned long long tl = __ballot(tiny != 0u);
             while (tl != 0ull) {
                 const int lp = __ffsll((long long)tl) - 1;  // uniform
@@ -139,7 +132,7 @@ __global__ __launch_bounds__(256) void cn_edge_kernel(DevGraph g, DevState st, A
                         double x = q;
                         if (lane == l) {
 #pragma unroll
-                            for (int i = 0; i < kEdgeKE; ++i)
+                            for (int i = 0; i < KE; ++i)
                                 if (i < nl && !(l == lp && i == ip)) x = x * t[i];
                         }
                         q = readlane_d(x, l);
@@ -147,20 +140,21 @@ __global__ __launch_bounds__(256) void cn_edge_kernel(DevGraph g, DevState st, A
                     if (lane == lp) {
                         const double v = 2.0 * atanh_f(clip_cl(q), ltab, ac);
 #pragma unroll
-                        for (int i = 0; i < kEdgeKE; ++i)
+                        for (int i = 0; i < KE; ++i)
                             if (i == ip) En[i] = v;
                     }
                 }
             }
         }
 #pragma unroll
-        for (int i = 0; i < kEdgeKE; ++i)
+        for (int i = 0; i < KE; ++i)
             if (i < nl) Ef[(size_t)(beg + p0 + i) * g.ef] = En[i];
     }
 }
 
 // One wavefront per (tile, column j), lanes over the column's edges (CSC
 // order: rows ascending), frame after frame: vn_cols_kernel's results.
+template <int KV>
 __global__ __launch_bounds__(256) void vn_edge_kernel(DevGraph g, DevState st, int nllr, uint32_t *zb, int *cnt,
                                                       int first) {
     const int tile = blockIdx.y;
@@ -168,30 +162,27 @@ __global__ __launch_bounds__(256) void vn_edge_kernel(DevGraph g, DevState st, i
     if (j >= g.n || !st.tile_active[tile]) return;
     const int lane = threadIdx.x & 63;
     const int p0 = g.csc_ptr[j], dc = g.csc_ptr[j + 1] - p0;
-    const int KV = max(1, (dc + 63) >> 6);
-    const int nlanes = (dc + KV - 1) / KV;
+    const int nlanes = (dc + KV - 1) / KV;  // (dc <= 64 KV: host check)
     const int q0 = lane * KV;
     const int nl = max(0, min(dc - q0, KV));
-    int ed[kEdgeKE];
+    int ed[KV];
 #pragma unroll
-    for (int i = 0; i < kEdgeKE; ++i)
-        if (i < KV) ed[i] = dc > 0 ? g.csc_edge[p0 + min(q0 + i, dc - 1)] : 0;
+    for (int i = 0; i < KV; ++i) ed[i] = dc > 0 ? g.csc_edge[p0 + min(q0 + i, dc - 1)] : 0;
     const int nw = (g.n + 31) >> 5;
     unsigned long long live = __ballot(st.done[tile * kTile + lane] == 0);
     while (live != 0ull) {
         const int f = __ffsll((long long)live) - 1;  // uniform
         live &= live - 1ull;
         const double *Ef = st.E + e_base(g, tile, f);
-        double v[kEdgeKE];
+        double v[KV];
 #pragma unroll
-        for (int i = 0; i < kEdgeKE; ++i)
-            if (i < KV) v[i] = dc > 0 ? Ef[(size_t)ed[i] * g.ef] : 0.0;
+        for (int i = 0; i < KV; ++i) v[i] = dc > 0 ? Ef[(size_t)ed[i] * g.ef] : 0.0;
         double s = 0.0;  // rows ascending, starting at 0.0
         for (int l = 0; l < nlanes; ++l) {
             double x = s;
             if (lane == l) {
 #pragma unroll
-                for (int i = 0; i < kEdgeKE; ++i)
+                for (int i = 0; i < KV; ++i)
                     if (i < nl) x = x + v[i];
             }
             s = readlane_d(x, l);
@@ -279,21 +270,40 @@ __global__ __launch_bounds__(256) void syn_row_kernel(DevGraph g, DevState st, c
 
 int edge_max_deg() { return 64 * kEdgeKE; }
 
+namespace {
+int edge_slots(int deg) { return deg <= 256 ? 4 : deg <= 512 ? 8 : deg <= 768 ? 12 : 16; }
+template <bool kFirst>
+void cn_edge_launch(const DevGraph &g, const DevState &st, hipStream_t s) {
+    const dim3 grid((unsigned)((g.m + 3) / 4), (unsigned)st.ntiles);
+    switch (edge_slots(g.max_row_deg)) {
+    case 4: cn_edge_kernel<kFirst, 4><<<grid, 256, 0, s>>>(g, st, kAtanhCoef); break;
+    case 8: cn_edge_kernel<kFirst, 8><<<grid, 256, 0, s>>>(g, st, kAtanhCoef); break;
+    case 12: cn_edge_kernel<kFirst, 12><<<grid, 256, 0, s>>>(g, st, kAtanhCoef); break;
+    default: cn_edge_kernel<kFirst, 16><<<grid, 256, 0, s>>>(g, st, kAtanhCoef); break;
+    }
+}
+}  // namespace
+
 hipError_t launch_cn_edge(const DevGraph &g, const DevState &st, int it, hipStream_t s) {
     if (g.max_row_deg > 64 * kEdgeKE) return hipErrorInvalidValue;
-    const dim3 grid((unsigned)((g.m + 3) / 4), (unsigned)st.ntiles);
     if (it == 0)
-        cn_edge_kernel<true><<<grid, 256, 0, s>>>(g, st, kAtanhCoef);
+        cn_edge_launch<true>(g, st, s);
     else
-        cn_edge_kernel<false><<<grid, 256, 0, s>>>(g, st, kAtanhCoef);
+        cn_edge_launch<false>(g, st, s);
     return hipGetLastError();
 }
 
 hipError_t launch_vn_edge_decode(const DevGraph &g, const DevState &st, int it, bool last, bool nllr, uint32_t *zb,
                                  int *cnt, int *bad, hipStream_t s) {
     if (!g.a_packed || g.max_col_deg > 64 * kEdgeKE || ((g.k + 31) >> 5) > kSynKw) return hipErrorInvalidValue;
-    vn_edge_kernel<<<dim3((unsigned)((g.n + 3) / 4), (unsigned)st.ntiles), 256, 0, s>>>(g, st, nllr ? 1 : 0, zb, cnt,
-                                                                                      it == 0 ? 1 : 0);
+    const dim3 vg((unsigned)((g.n + 3) / 4), (unsigned)st.ntiles);
+    const int nl = nllr ? 1 : 0, fi = it == 0 ? 1 : 0;
+    switch (edge_slots(g.max_col_deg)) {
+    case 4: vn_edge_kernel<4><<<vg, 256, 0, s>>>(g, st, nl, zb, cnt, fi); break;
+    case 8: vn_edge_kernel<8><<<vg, 256, 0, s>>>(g, st, nl, zb, cnt, fi); break;
+    case 12: vn_edge_kernel<12><<<vg, 256, 0, s>>>(g, st, nl, zb, cnt, fi); break;
+    default: vn_edge_kernel<16><<<vg, 256, 0, s>>>(g, st, nl, zb, cnt, fi); break;
+    }
     if (st.count <= kSynRowFrames) {
         const int waves = (g.m + 63) / 64;
         syn_row_kernel<<<dim3((unsigned)((waves + 3) / 4), (unsigned)st.ntiles), 256, 0, s>>>(g, st, zb, bad);
