@@ -279,7 +279,7 @@ bool small_batch_cols(const DevGraph &G, int ntiles) {
 // Few frames: the lanes of a wavefront take a row's / column's edges instead
 // of frames (edge_kernels.hip), so a pass's loads are all in flight at once --
 // main.py's one-frame decode() calls: one wimax_2304_0.5 frame at T=50 in
-// 5.1 ms instead of 102 ms, 8 frames in 20 ms (a frame costs ~2 ms more;
+// 5.1 ms instead of 102 ms (4.3 ms since), 8 frames in 20 ms (a frame costs ~2 ms more;
 // profiles/r3g_edge).  LDPC_EDGE_FRAMES (read per call): the batch size up to
 // which it applies (default 32 for the 2304 codes, below the frame-per-lane
 // path's ~100 ms; 4 for the codes of the 64-frame tile_kernel, whose one
