@@ -87,8 +87,19 @@ def parse():
     ap.add_argument("--phys-steps", type=int, default=4,
                     help="parity mode: timed physical-mode steps reported under 'physical' after the "
                          "headline (0 = none); not the reference's arithmetic (SURVEY 8 f4)")
+    ap.add_argument("--phys-waterfall-snr", type=float, default=-2.5,
+                    help="parity mode: a second physical-mode point in the waterfall, where the decoder "
+                         "iterates (reported under physical.waterfall; NaN = none)")
     ap.add_argument("--phys-frames", type=int, default=262144,
                     help="frames per physical-mode step (config 3's batch; 65,536 measured 2.7 % slower: host syncs)")
+    ap.add_argument("--config4-snr", default="1.0:0.5:4.0",
+                    help="parity mode: BASELINE config 4's Eb/N0 sweep (start:step:end, main.py's grid) on "
+                         "--config4-code, reported under 'config4' ('' = none)")
+    ap.add_argument("--config4-code", default="wimax_2304_0.75A")
+    ap.add_argument("--config4-frames", type=int, default=32768,
+                    help="frames per GPU per config-4 point (one GPU's shard of 262,144 over 8 GPUs)")
+    ap.add_argument("--config4-slots", type=int, default=2048,
+                    help="streaming slots of the config-4 decoder (256 CUs x one 8-frame tile8 workgroup)")
     ap.add_argument("--dropin-calls", type=int, default=20,
                     help="parity mode: one-frame decode() calls timed under 'dropin' (main.py's call pattern; 0 = none)")
     ap.add_argument("--stub", action="store_true",
@@ -212,16 +223,25 @@ def max_over_ranks(dist, x, local):
 VALU_PEAK = 256 * 4 * 2.4e9 / 2.0  # wave64 VALU instructions/s (2 cycles each per SIMD)
 
 
-def committed_valu(code, kernel):
-    """VALU wave-instructions per frame-iteration of `kernel` on `code` from the
-    newest committed profile (tools/profile_phys.sh + summarize_phys_profile.py)."""
+def committed_valu(code, kernel, snr_db):
+    """VALU wave-instructions per frame-iteration of `kernel` on `code` at this
+    SNR from the newest committed profile (tools/profile_phys.sh +
+    summarize_phys_profile.py: profiles/<tag>/valu*.json).  The count per
+    frame-iteration depends on the operating point (per-pass overheads are
+    shared by fewer iterations when frames stop early), so only a profile of
+    the same SNR counts."""
     pdir = os.path.join(ROOT, "profiles")
     best = (None, None)
     for d in sorted(os.listdir(pdir), key=profile_order) if os.path.isdir(pdir) else []:
-        f = os.path.join(pdir, d, "valu.json")
-        if os.path.exists(f):
+        if not os.path.isdir(os.path.join(pdir, d)):
+            continue
+        for fn in sorted(os.listdir(os.path.join(pdir, d))):
+            if not (fn.startswith("valu") and fn.endswith(".json")):
+                continue
+            f = os.path.join(pdir, d, fn)
             v = json.load(open(f))
-            if v.get("code") == code and v.get("kernel") == kernel:
+            if v.get("code") == code and v.get("kernel") == kernel and \
+                    abs(float(v.get("snr_db", 1e9)) - snr_db) < 1e-9:
                 best = (v["valu_insts_per_frame_iteration"], os.path.relpath(f, ROOT))
     return best
 
@@ -344,54 +364,170 @@ def physical_extra(args, edd, graph, local, world, rank, dist, k):
     8 f4): standard SPA on the sparse graph H[:, perm], sign-consistent, fp32,
     a frame's state in LDS.  NOT the reference's arithmetic (no parity): timed
     here after the parity headline, outside its timed region, over the same
-    code, max_iter, SNR and on-device frame source, on frame indices disjoint
-    from the headline's.  Roofline = VALU issue (the state never leaves LDS):
-    committed PMC VALU instructions per frame-iteration of the same kernel and
-    code x this run's frame-iterations / the kernel's HIP-event time."""
+    code, max_iter and on-device frame source, on frame indices disjoint from
+    the headline's -- at the headline's SNR (1 dB on the reference axis, where
+    the reference channel's noise std sigma^2 makes frames converge in ~1
+    iteration) and at a waterfall point (--phys-waterfall-snr, -2.5 dB: ~35
+    iterations, FER ~0.4) where the decoder actually iterates.  Roofline = VALU
+    issue (the state never leaves LDS): committed PMC VALU instructions per
+    frame-iteration of the same kernel, code and SNR x this run's
+    frame-iterations / the kernel's HIP-event time."""
     from ldpc_amd import _lib
     from ldpc_amd.device import Decoder, Graph
     pg = Graph(edd.physical_matrix(), device=local)
     B = args.phys_frames
     pdec = Decoder(graph, B)  # frame source = H_std; E is never allocated in physical mode
-    sig = 1.0 / math.sqrt(2.0 * 1.0 * (10.0 ** (args.snr * 0.1)))
-    base = 1 << 42  # far from the parity steps' frame ranges
-    pdec.phys_mc_run(pg, SEED, [sig], B, base + rank * B, args.iters)  # untimed warm-up
-    barrier(dist, local)
-    pdec.profile_read()
-    pdec.profile(True)
-    barrier(dist, local)
-    t0 = time.perf_counter()
-    loc = np.zeros((1, 7), np.int64)
-    tot = np.zeros((1, 7), np.int64)
-    for s in range(args.phys_steps):
-        c = pdec.phys_mc_run(pg, SEED, [sig], B, base + ((s + 1) * world + rank) * B, args.iters)
-        loc += c
-        tot += allreduce_counters(dist, c, local)
-    barrier(dist, local)
-    dt = max_over_ranks(dist, time.perf_counter() - t0, local)
-    pdec.profile(False)
-    prof = pdec.profile_read()
-    pms, pl = prof["phys"]
     name = _lib.lib().ldpc_phys_kernel_name(pg.handle, 0).decode()
-    frames = int(tot[0, 0])
+
+    def point(snr, base):
+        sig = 1.0 / math.sqrt(2.0 * 1.0 * (10.0 ** (snr * 0.1)))
+        pdec.phys_mc_run(pg, SEED, [sig], B, base + rank * B, args.iters)  # untimed warm-up
+        barrier(dist, local)
+        pdec.profile_read()
+        pdec.profile(True)
+        barrier(dist, local)
+        t0 = time.perf_counter()
+        loc = np.zeros((1, 7), np.int64)
+        tot = np.zeros((1, 7), np.int64)
+        for s in range(args.phys_steps):
+            c = pdec.phys_mc_run(pg, SEED, [sig], B, base + ((s + 1) * world + rank) * B, args.iters)
+            loc += c
+            tot += allreduce_counters(dist, c, local)
+        barrier(dist, local)
+        dt = max_over_ranks(dist, time.perf_counter() - t0, local)
+        pdec.profile(False)
+        pms, pl = pdec.profile_read()["phys"]
+        frames = int(tot[0, 0])
+        out = {"value": frames / dt, "unit": "codewords/s", "per_gpu": frames / dt / world, "n_gpus": world,
+               "steps": args.phys_steps, "frames_per_gpu_step": B, "ms_per_step": dt / args.phys_steps * 1e3,
+               "info_bits_per_s": frames * k / dt, "dtype": "f32", "snr_db": snr, "max_iter": args.iters,
+               "edges_H_phys": int(pg.nnz), "fer": int(tot[0, 1]) / max(frames, 1),
+               "ber": int(tot[0, 2]) / (k * max(frames, 1)), "avg_iters": int(tot[0, 6]) / max(frames, 1),
+               "kernel": name, "kernel_ms": pms, "launches": pl}
+        vi, vsrc = committed_valu(args.code, name, snr)
+        if vi and pms:
+            ach = vi * int(loc[0, 6]) / (pms / 1e3)
+            out["roofline"] = {"bound": "valu", "achieved": ach, "peak": VALU_PEAK, "unit": "VALU wave-instr/s",
+                               "frac": ach / VALU_PEAK, "valu_insts_per_frame_iteration": vi, "valu_source": vsrc,
+                               "peak_model": "256 CUs x 4 SIMDs x 2.4 GHz / 2 cycles per wave64 fp32 VALU "
+                                             "instruction (MI355X_MICROARCH.md)"}
+        return out
+
     out = {"what": "physical mode (SURVEY 8 f4): standard SPA on the sparse H[:,perm], sign-consistent, fp32, "
                    "state in LDS -- NOT the reference's arithmetic, no parity with spa_decoder.py; timed after "
                    "and outside the parity headline",
-           "value": frames / dt, "unit": "codewords/s", "per_gpu": frames / dt / world, "n_gpus": world,
-           "steps": args.phys_steps, "frames_per_gpu_step": B, "ms_per_step": dt / args.phys_steps * 1e3,
-           "info_bits_per_s": frames * k / dt, "dtype": "f32", "snr_db": args.snr, "max_iter": args.iters,
-           "edges_H_phys": int(pg.nnz), "fer": int(tot[0, 1]) / max(frames, 1),
-           "ber": int(tot[0, 2]) / (k * max(frames, 1)), "avg_iters": int(tot[0, 6]) / max(frames, 1),
-           "kernel": name, "kernel_ms": pms, "launches": pl,
            "north_star_target_cw_s_8gpu": 1e8}
-    vi, vsrc = committed_valu(args.code, name)
-    if vi and pms:
-        ach = vi * int(loc[0, 6]) / (pms / 1e3)
-        out["roofline"] = {"bound": "valu", "achieved": ach, "peak": VALU_PEAK, "unit": "VALU wave-instr/s",
-                           "frac": ach / VALU_PEAK, "valu_insts_per_frame_iteration": vi, "valu_source": vsrc,
-                           "peak_model": "256 CUs x 4 SIMDs x 2.4 GHz / 2 cycles per wave64 fp32 VALU "
-                                         "instruction (MI355X_MICROARCH.md)"}
+    out.update(point(args.snr, 1 << 42))  # far from the parity steps' frame ranges
+    if not math.isnan(args.phys_waterfall_snr):
+        out["waterfall"] = point(args.phys_waterfall_snr, (1 << 42) + (1 << 38))
     pdec.close()
+    return out
+
+
+def snr_grid(spec):
+    """main.py's SNR grid (main.py:193,206-209): steps = ceil((end - start) / step) + 1,
+    the last point clamped to end.  spec 'start:step:end' or a comma list."""
+    if ":" not in spec:
+        return [float(v) for v in spec.split(",") if v.strip()]
+    a, st, b = (float(v) for v in spec.split(":"))
+    n = int(math.ceil((b - a) / st)) + 1
+    return [round(min(a + i * st, b), 10) for i in range(n)]
+
+
+def config4_extra(args, local, world, rank, dist):
+    """BASELINE config 4: wimax_2304_0.75A, Eb/N0 sweep 1.0..4.0 dB, T=50 with
+    early termination, frames sharded over the GPUs (this rank: its own
+    --config4-frames per point, disjoint global frame ranges) with the counter
+    all-reduce per point.  Each point is ONE streaming mc_run call: the
+    8-frame sub-tile decoder tile8_stream_kernel (per-slot refill by gen_slots)
+    with the hand-off of its last running frames to the column-parallel split
+    tail.  Per point: cw/s, the main.py counters, and the whole decode's
+    algorithmic bytes (8 n + 16 B x edges x iterations + ceil(n/8) +
+    8 per frame) over the decode kernels' HIP-event time (stream kernel + tail
+    CN/VN + refills).  Then one static 32,768-frame step at 1 dB through
+    tile8_kernel (every frame runs 50 iterations there), the r3/4 decoder's
+    fused-kernel roofline like the headline's."""
+    import ldpc_amd
+    from ldpc_amd import _lib
+    from ldpc_amd.device import Decoder, Graph
+    edd = ldpc_amd.load_committed_code(args.config4_code)
+    H = edd._h_std
+    n, k, nnz = edd._n, edd._k, H.nnz
+    g = Graph(H, device=local)
+    F = args.config4_frames
+    dec = Decoder(g, min(args.config4_slots, F))
+    sig = lambda x: 1.0 / math.sqrt(2.0 * 1.0 * (10.0 ** (x * 0.1)))  # noqa: E731  channel.py:113
+    base = 1 << 43  # far from every other key's frame ranges
+    dec.mc_run(SEED, [sig(2.5)], 256, base - 4096, args.iters)  # untimed warm-up (workspace, first launches)
+    pts, tot_f, tot_t, tot_b, tot_ms = [], 0, 0.0, 0.0, 0.0
+    kinds = ("tile", "cn", "vn", "vn_cols", "generate")
+    for i, x in enumerate(snr_grid(args.config4_snr)):
+        barrier(dist, local)
+        dec.profile_read()
+        dec.profile(True)
+        t1 = time.perf_counter()
+        loc = dec.mc_run(SEED, [sig(x)], F, base + (i * world + rank) * F, args.iters)
+        c = allreduce_counters(dist, loc, local)
+        barrier(dist, local)
+        dt = max_over_ranks(dist, time.perf_counter() - t1, local)
+        dec.profile(False)
+        prof = dec.profile_read()
+        f = int(c[0, 0])
+        ms = sum(prof[kk][0] for kk in kinds)
+        byts = F * (8 * n + math.ceil(n / 8) + 8) + 16.0 * nnz * int(loc[0, 6])  # this rank
+        pts.append({"snr_db": x, "value": f / dt, "unit": "codewords/s", "info_bits_per_s": f * k / dt,
+                    "ms": dt * 1e3, "frames": f, "avg_iters": int(c[0, 6]) / max(f, 1),
+                    "fer": int(c[0, 1]) / max(f, 1), "ber": int(c[0, 2]) / (k * max(f, 1)),
+                    "decode_ms": ms, "stream_kernel_ms": prof["tile"][0],
+                    "tail_ms": prof["cn"][0] + prof["vn"][0] + prof["vn_cols"][0],
+                    "roofline_frac": byts / (ms / 1e3) / 1e9 / HBM_PEAK_GBS if ms else None})
+        tot_f += f
+        tot_t += dt
+        tot_b += byts
+        tot_ms += ms
+    dec.close()
+    out = {"what": "BASELINE config 4: Eb/N0 sweep, one streaming mc_run per point (tile8_stream_kernel + "
+                   "column-parallel tail), counters all-reduced per point",
+           "code": args.config4_code, "n": n, "k": k, "edges_H_std": nnz, "max_iter": args.iters,
+           "frames_per_gpu_per_point": F, "slots": min(args.config4_slots, F), "n_gpus": world,
+           "kernel": _lib.lib().ldpc_tile_kernel_name(g.handle).decode().replace("_kernel", "_stream_kernel"),
+           "value": tot_f / tot_t, "unit": "codewords/s", "info_bits_per_s": tot_f * k / tot_t,
+           "points": pts,
+           "roofline": {"bound": "hbm", "achieved": tot_b / (tot_ms / 1e3) / 1e9, "peak": HBM_PEAK_GBS,
+                        "unit": "GB/s", "frac": tot_b / (tot_ms / 1e3) / 1e9 / HBM_PEAK_GBS,
+                        "bytes_model": "whole sweep, this rank: per frame 8 n + 16 B x H_std edges x iterations "
+                                       "executed + ceil(n/8) + 8 (SURVEY 8d), over the decode kernels' HIP-event "
+                                       "time (stream kernel + tail + refills)"}}
+    tr, tsrc = committed_traffic(nnz, min(args.config4_slots, F), "tile8_stream")
+    if tr is not None:
+        out["roofline"]["traffic"] = tr
+        out["roofline"]["traffic_source"] = tsrc
+    # the fused static decoder (tile8_kernel) at 1 dB: one 32,768-frame launch, all 50 iterations
+    sdec = Decoder(g, F)
+    sdec.mc_run(SEED, [sig(1.0)], F, base - 2 * F - 4096, args.iters, static=True)  # warm-up
+    barrier(dist, local)
+    sdec.profile_read()
+    sdec.profile(True)
+    t1 = time.perf_counter()
+    loc = sdec.mc_run(SEED, [sig(1.0)], F, base + (1 << 40) + rank * F, args.iters, static=True)
+    c = allreduce_counters(dist, loc, local)
+    barrier(dist, local)
+    dt = max_over_ranks(dist, time.perf_counter() - t1, local)
+    sdec.profile(False)
+    prof = sdec.profile_read()
+    sdec.close()
+    tms, tl = prof["tile"]
+    byts = F * (8 * n + math.ceil(n / 8) + 8) + 16.0 * nnz * int(loc[0, 6])
+    st = {"snr_db": 1.0, "schedule": "static", "frames": int(c[0, 0]), "value": int(c[0, 0]) / dt,
+          "unit": "codewords/s", "avg_iters": int(c[0, 6]) / max(int(c[0, 0]), 1),
+          "kernel": _lib.lib().ldpc_tile_kernel_name(g.handle).decode(), "launches": tl,
+          "avg_launch_ms": tms / max(tl, 1)}
+    if tl:
+        st["roofline"] = {"bound": "hbm", "achieved": byts / (tms / 1e3) / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                          "frac": byts / (tms / 1e3) / 1e9 / HBM_PEAK_GBS, "bytes_per_launch": byts / tl}
+        tr, tsrc = committed_traffic(nnz, F, "tile")
+        st["roofline"]["traffic"], st["roofline"]["traffic_source"] = tr, tsrc
+    out["static_1dB"] = st
     return out
 
 
@@ -430,8 +566,13 @@ def main():
     if not launched and args.gpus > 1:
         sys.exit(self_launch(args, sys.argv[1:]))  # nothing has touched HIP in this process
     world = int(os.environ.get("WORLD_SIZE", "1"))
-    if world != args.gpus:
+    if world < args.gpus:  # fewer ranks than asked for: never report a smaller job as the N-GPU one
         raise SystemExit(f"bench.py: --gpus {args.gpus} but the launcher started WORLD_SIZE={world} ranks")
+    if world > args.gpus:  # e.g. torchrun --nproc-per-node 8 bench.py without --gpus: the launcher's world rules
+        if int(os.environ.get("RANK", "0")) == 0:
+            print(f"bench.py: WORLD_SIZE={world} from the launcher, --gpus {args.gpus}: running {world} ranks",
+                  file=sys.stderr)
+        args.gpus = world
     if args.stub or os.environ.get("LDPC_BENCH_STUB") == "1":
         return stub_rank(args, world, int(os.environ.get("RANK", "0")))
     import ldpc_amd
@@ -569,6 +710,10 @@ def main():
     if args.phys_steps > 0 and pgraph is None and not ira_code:
         dec.close()
         physical = physical_extra(args, edd, graph, local, world, rank, dist, k)
+    config4 = None
+    if args.config4_snr.strip() and pgraph is None and not ira_code:
+        dec.close()  # idempotent (the physical key may have closed it)
+        config4 = config4_extra(args, local, world, rank, dist)
     dropin = dropin_extra(args, graph, n) if args.dropin_calls > 0 and pgraph is None else None
 
     frames_total = int(totals[0, 0])
@@ -643,6 +788,8 @@ def main():
         out["snr_points"] = snr_points
     if physical is not None:
         out["physical"] = physical
+    if config4 is not None:
+        out["config4"] = config4
     if dropin is not None:
         out["dropin"] = dropin
     if not tile_launches and pgraph is None and cn_launches:
@@ -718,7 +865,7 @@ def main():
             out["roofline"] = {"bound": "valu", "kernel": pname, "launches": pl,
                                "avg_launch_ms": pms / max(pl, 1),
                                "note": "state in LDS; HBM traffic is the frame input only"}
-            vi, vsrc = committed_valu(args.code, pname)
+            vi, vsrc = committed_valu(args.code, pname, args.snr)
             if vi and pms:
                 # VALU issue roofline: wave-instructions per frame-iteration (committed PMC of the
                 # same kernel and code) x this run's frame-iterations / the kernel's HIP-event time

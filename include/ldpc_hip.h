@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define LDPC_ABI_VERSION 3  /* 3: ldpc_diag_tile_trace removed */
+#define LDPC_ABI_VERSION 4  /* 4: profile kinds of the few-frame / column-parallel kernels (LDPC_K_NKINDS 11) */
 
 /* error codes */
 #define LDPC_OK 0
@@ -97,8 +97,10 @@ const char *ldpc_cn_kernel_name(const ldpc_graph *g);
  * the static schedule of ldpc_mc_run decode a whole chunk in ONE launch; the
  * separate per-iteration launches remain available via LDPC_F_SPLIT. */
 int64_t ldpc_tile_lds_bytes(const ldpc_graph *g);
-/* "tile_kernel" (64 frames per workgroup), "tile_sub_kernel" (16 or 8), or ""
- * when the tile-resident decoder does not apply -- measurement label. */
+/* The tile-resident decoder this graph runs -- "tile_kernel" (64 frames per
+ * workgroup), "tile_sub_kernel" (16 frames: wimax_2304_0.5) or "tile8_kernel"
+ * (8 frames: the r3/4 codes, or any 2304 code whose graph was created with
+ * LDPC_TILE8=1) -- or "" when it does not apply; measurement label. */
 const char *ldpc_tile_kernel_name(const ldpc_graph *g);
 /* Physical-mode kernel for this (sparse) graph: "phys_reg_kernel" / "phys_kernel"
  * (state in LDS) or "phys_cn_tile_kernel" (state in HBM). */
@@ -204,15 +206,19 @@ int ldpc_phys_mc_run(ldpc_decoder *d_std, const ldpc_graph *g_phys, uint64_t see
  * synchronises, returns the summed milliseconds and launch counts per kind
  * (LDPC_K_*), and resets the accumulators.
  */
-#define LDPC_K_CN 0
-#define LDPC_K_VN 1
+#define LDPC_K_CN 0      /* cn_kernel / cn_row_kernel (+ cn_rare_kernel): the split path's CN */
+#define LDPC_K_VN 1      /* vn_kernel: the split path's per-tile VN */
 #define LDPC_K_GEN 2
 #define LDPC_K_COUNT 3
 #define LDPC_K_PHYS 4
 #define LDPC_K_PHYS_CN 5
 #define LDPC_K_PHYS_VN 6
-#define LDPC_K_TILE 7 /* tile-resident decoder: all iterations of a chunk */
-#define LDPC_K_NKINDS 8
+#define LDPC_K_TILE 7 /* tile-resident decoder: all iterations of a chunk (or a streamed SNR point) */
+#define LDPC_K_CN_EDGE 8  /* few-frame path: cn_edge_kernel (lanes over a row's edges) */
+#define LDPC_K_VN_EDGE 9  /* few-frame path: vn_edge_kernel + syn_kernel + tail_exit_kernel */
+#define LDPC_K_VN_COLS 10 /* column-parallel VN: vn_cols_kernel + tail_exit_kernel (small batches,
+                             streaming tail) */
+#define LDPC_K_NKINDS 11
 int ldpc_profile_enable(ldpc_decoder *d, int enable);
 int ldpc_profile_read(ldpc_decoder *d, double *ms_out, int64_t *launches_out);
 

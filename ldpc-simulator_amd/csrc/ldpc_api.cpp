@@ -293,13 +293,19 @@ bool small_batch_edge(const DevGraph &G, int count) {
     return count <= lim && G.max_row_deg <= ldpc::edge_max_deg() && G.max_col_deg <= ldpc::edge_max_deg();
 }
 
-// the column-parallel VN's per-tile buffers (zero between passes)
+// the column-parallel VN's per-tile buffers (zero between passes).  Each
+// buffer is allocated under its own null check, so a failed allocation leaves
+// the others consistent and a later call retries only what is missing.
 int ensure_tail_bufs(ldpc_decoder *d, hipStream_t s) {
     const DevGraph &G = d->g->dg;
     const int cap = d->cap_tiles * kTile;
     const size_t nzb = (size_t)d->cap_tiles * ((G.n + 31) / 32) * kTile;
-    if (!d->tzb && (dev_alloc(&d->tzb, nzb) || dev_alloc(&d->tcnt, (size_t)cap) || dev_alloc(&d->tbad, (size_t)cap)))
-        return LDPC_ENOMEM;
+    if (!d->tzb)
+        if (int rc = dev_alloc(&d->tzb, nzb)) return rc;
+    if (!d->tcnt)
+        if (int rc = dev_alloc(&d->tcnt, (size_t)cap)) return rc;
+    if (!d->tbad)
+        if (int rc = dev_alloc(&d->tbad, (size_t)cap)) return rc;
     // tail_exit_kernel leaves them zero, but a call that stopped early (an
     // error return) may not have: cleared per call, never trusted
     if (hipMemsetAsync(d->tzb, 0, nzb * sizeof(uint32_t), s) != hipSuccess ||
@@ -312,47 +318,61 @@ int ensure_tail_bufs(ldpc_decoder *d, hipStream_t s) {
 // Up to max_iter CN/VN sweeps.  With poll (callers that synchronise anyway),
 // the host reads how many tiles are still running after VN(it) for it < 4 and
 // every 4th iteration after, and stops once none is: launches over finished
-// tiles cost ~0.3 ms each (a grid of early-exiting workgroups).
-hipError_t run_iterations(ldpc_decoder *d, const DevGraph &G, const DevState &st_in, int max_iter, bool nllr,
-                          hipStream_t s, bool poll, bool split) {
-    hipError_t e = hipSuccess;
+// tiles cost ~0.3 ms each (a grid of early-exiting workgroups).  Which path
+// runs is decided first (few-frame edge path, small-batch column-parallel VN,
+// the tile-resident decoder, or the split CN/VN launches); an allocation or
+// HIP failure is returned as an LDPC_E* code, never turned into another path.
+int run_iterations(ldpc_decoder *d, const DevGraph &G, const DevState &st_in, int max_iter, bool nllr,
+                   hipStream_t s, bool poll, bool split) {
     DevState st = st_in;
     // the edge path applies to every [A | I] code with k <= 2048 (the 64-frame
     // tile codes too: one wimax_576_0.5 frame, profiles/r3g_edge)
-    const bool edge = G.a_packed && ((G.k + 31) >> 5) <= 64 && tail_vn_enabled() && small_batch_edge(G, st.count) &&
-                      ensure_tail_bufs(d, s) == LDPC_OK;
-    const bool cols = edge || (small_batch_cols(G, st.ntiles) && ensure_tail_bufs(d, s) == LDPC_OK);
+    const bool cols_ok = G.a_packed && ((G.k + 31) >> 5) <= 64 && tail_vn_enabled();
+    const bool edge = cols_ok && small_batch_edge(G, st.count);
+    const bool cols = edge || (cols_ok && small_batch_cols(G, st.ntiles));
+    if (cols)
+        if (int rc = ensure_tail_bufs(d, s)) return rc;
+    auto hip = [](hipError_t e) {
+        return e == hipSuccess ? LDPC_OK
+                               : ldpc_fail(LDPC_EDEVICE, "decode iterations: %s", hipGetErrorString(e));
+    };
     if (!split && !cols && ldpc::use_tile(G) && st.ntiles <= st.nslots)  // one launch: every tile to its own exit
-        return timed(d, LDPC_K_TILE, s, [&] { return ldpc::launch_tile(G, st, max_iter, nllr, s); });
+        return hip(timed(d, LDPC_K_TILE, s, [&] { return ldpc::launch_tile(G, st, max_iter, nllr, s); }));
     // cn_rare_kernel clears the OTHER parity's count for the next CN; the one
     // the last iteration used (or an early stop left) is cleared here
-    if ((e = hipMemsetAsync(st.rare_count, 0, sizeof(int) * 2, s))) return e;
+    hipError_t e = hipMemsetAsync(st.rare_count, 0, sizeof(int) * 2, s);
+    if (e) return hip(e);
     if (poll) {
         if (d->pactive_cap < max_iter) {
             (void)hipFree(d->pactive);
             d->pactive = nullptr;
             d->pactive_cap = 0;
-            if (hipMalloc((void **)&d->pactive, sizeof(int) * max_iter) != hipSuccess) return hipErrorOutOfMemory;
+            if (int rc = dev_alloc(&d->pactive, (size_t)max_iter)) return rc;
             d->pactive_cap = max_iter;
         }
-        if ((e = hipMemsetAsync(d->pactive, 0, sizeof(int) * max_iter, s))) return e;
+        if ((e = hipMemsetAsync(d->pactive, 0, sizeof(int) * max_iter, s))) return hip(e);
         st.active_count = d->pactive;
     }
     for (int it = 0; it < max_iter && e == hipSuccess; ++it) {
         if (edge) {  // the rare rows are handled inside cn_edge_kernel
-            e = timed(d, LDPC_K_CN, s, [&] { return ldpc::launch_cn_edge(G, st, it, s); });
+            e = timed(d, LDPC_K_CN_EDGE, s, [&] { return ldpc::launch_cn_edge(G, st, it, s); });
         } else {
             e = timed(d, LDPC_K_CN, s, [&] { return ldpc::launch_cn(G, st, it, s); });
             if (e == hipSuccess) e = ldpc::launch_cn_rare(G, st, it, s);
         }
-        if (e == hipSuccess)
-            e = timed(d, LDPC_K_VN, s, [&] {
-                if (edge)
-                    return ldpc::launch_vn_edge_decode(G, st, it, it + 1 == max_iter, nllr, d->tzb, d->tcnt, d->tbad,
-                                                       s);
-                return cols ? ldpc::launch_vn_cols_decode(G, st, it, it + 1 == max_iter, nllr, d->tzb, d->tcnt, s)
-                            : ldpc::launch_vn(G, st, it, max_iter, nllr, s);
-            });
+        if (e == hipSuccess) {
+            const bool last = it + 1 == max_iter;
+            if (edge)
+                e = timed(d, LDPC_K_VN_EDGE, s, [&] {
+                    return ldpc::launch_vn_edge_decode(G, st, it, last, nllr, d->tzb, d->tcnt, d->tbad, s);
+                });
+            else if (cols)
+                e = timed(d, LDPC_K_VN_COLS, s, [&] {
+                    return ldpc::launch_vn_cols_decode(G, st, it, last, nllr, d->tzb, d->tcnt, s);
+                });
+            else
+                e = timed(d, LDPC_K_VN, s, [&] { return ldpc::launch_vn(G, st, it, max_iter, nllr, s); });
+        }
         if (e == hipSuccess && poll && it + 1 < max_iter && (it < 4 || (it + 1) % 4 == 0)) {
             int running = 0;
             e = hipMemcpyAsync(&running, d->pactive + it, sizeof(int), hipMemcpyDeviceToHost, s);
@@ -360,7 +380,7 @@ hipError_t run_iterations(ldpc_decoder *d, const DevGraph &G, const DevState &st
             if (e == hipSuccess && running == 0) break;
         }
     }
-    return e;
+    return hip(e);
 }
 
 // cn_rare_kernel runs 1024 blocks x 4 wavefronts; one scratch slot each.
@@ -379,6 +399,10 @@ size_t workspace_bytes(const DevGraph &g, int cap_tiles) {
     b += cap * kw * 4;                 // ubits
     b += 2 * cap * (size_t)g.n * 8;    // llr/post staging
     b += cap * (size_t)g.n;            // z staging
+    b += cap * ((size_t)(g.n + 31) / 32) * 4 + 2 * cap * 4;  // column-parallel VN / few-frame buffers (tzb, tcnt, tbad)
+    // not included: the normalized-LLR history of decode() calls that ask for
+    // it (cap x max_iter doubles, allocated on first use, grow-only) and the
+    // Monte-Carlo counters (7 int64 per SNR point)
     return b;
 }
 
@@ -709,8 +733,10 @@ int ldpc_decode_f64(ldpc_decoder *d, int32_t batch, const double *llr, int32_t m
         }
         if ((e = ldpc::launch_reset(G, st, s))) return fail_dev(e, "reset");
         if ((e = ldpc::launch_load_llr(G, st, src, s))) return fail_dev(e, "load");
-        if ((e = run_iterations(d, G, st, max_iter, nllr, s, !dev_ptrs, flags & LDPC_F_SPLIT)))
-            return fail_dev(e, "iteration");
+        if (int rc1 = run_iterations(d, G, st, max_iter, nllr, s, !dev_ptrs, flags & LDPC_F_SPLIT)) {
+            (void)hipFree(d_msgs);
+            return rc1;
+        }
         uint8_t *zdst = dev_ptrs ? (z_out ? z_out + (size_t)start * n : nullptr) : d->z_stage;
         double *pdst = dev_ptrs ? (post_out ? post_out + (size_t)start * n : nullptr) : (post_out ? d->post_stage : nullptr);
         if (zdst || pdst) {
@@ -837,12 +863,14 @@ bool tail_vn_enabled() {
 // step takes 615 ms instead of 1.1 s; at 2 dB, where nearly every slot runs to
 // 50 passes, the sub-tile kernel keeps the bulk (3/4: -2 % there;
 // profiles/r2au_tail).
-int64_t handoff_frames(int64_t slots) {
+// fpw: frames per workgroup of the streaming sub-tile kernel (16, or 8 for
+// tile8_stream_kernel), one workgroup per CU.
+int64_t handoff_frames(int64_t slots, int fpw) {
     const char *e = getenv("LDPC_HANDOFF");
     if (e) return atoll(e);
     int dev = 0, cus = 256;
     if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    return std::min<int64_t>(slots, (int64_t)cus * 16) * 3 / 5;
+    return std::min<int64_t>(slots, (int64_t)cus * fpw) * 3 / 5;
 }
 
 // Streaming schedule of one SNR point: the decoder's cap frames are slots.  A
@@ -873,7 +901,8 @@ int mc_stream_point(ldpc_decoder *d, uint64_t seed, int p, double sigma, int64_t
         // one launch: every workgroup's lanes pull frames until the supply is
         // out; the sub-tile decoder hands its last running frames to the
         // column-parallel tail below (one pass of a sub-tile costs ~14 ms)
-        const int64_t ho = tail_ok && ldpc::sub_frames(G) == 16 ? handoff_frames((int64_t)ntiles * kTile) : 0;
+        const int fpw = G.ef == 8 ? 8 : ldpc::sub_frames(G) == 16 ? 16 : 0;  // 0: tile_stream_kernel, no hand-off
+        const int64_t ho = tail_ok && fpw ? handoff_frames((int64_t)ntiles * kTile, fpw) : 0;
         HIP_TRY(hipMemsetAsync(next, 0, sizeof(unsigned long long), s));
         HIP_TRY(timed(d, LDPC_K_TILE, s, [&] {
             return ldpc::launch_tile_stream(G, st, max_iter, nllr, seed, p, sigma, frame0, total, next, ctr, ho, s);
@@ -925,7 +954,7 @@ int mc_stream_point(ldpc_decoder *d, uint64_t seed, int p, double sigma, int64_t
             HIP_TRY(timed(d, LDPC_K_CN, s, [&] { return ldpc::launch_cn(G, st, par, s, true); }));
             HIP_TRY(ldpc::launch_cn_rare(G, st, par, s, true));
             if (tail_ok && cur <= kTailTiles)
-                HIP_TRY(timed(d, LDPC_K_VN, s,
+                HIP_TRY(timed(d, LDPC_K_VN_COLS, s,
                               [&] { return ldpc::launch_vn_tail(G, st, max_iter, nllr, d->tzb, d->tcnt, ctr, s); }));
             else
                 HIP_TRY(timed(d, LDPC_K_VN, s, [&] { return ldpc::launch_vn(G, st, 0, max_iter, nllr, s, ctr); }));
@@ -985,22 +1014,22 @@ int ldpc_mc_run(ldpc_decoder *d, uint64_t seed, int32_t n_points, const double *
                                          flags & LDPC_F_SPLIT, s))
                 return rc;
     } else {
-    if (int rc = ensure_pbits(d, G)) return rc;
-    for (int p = 0; p < n_points; ++p) {
-        for (int64_t start = 0; start < frames_per_point; start += cap) {
-            const int cnt = (int)std::min<int64_t>(cap, frames_per_point - start);
-            state_bind(d, (cnt + kTile - 1) / kTile, cnt);
-            HIP_TRY(ldpc::launch_reset(G, d->st, s));
-            const DevState st = d->st;
-            HIP_TRY(timed(d, LDPC_K_GEN, s,
-                          [&] { return ldpc::launch_frames(G, st, phys_tile(d), seed, p, sigmas[p], frame0 + start,
-                                                           ldpc::kFramesCh, nullptr, s); }));
-            HIP_TRY(run_iterations(d, G, st, max_iter, nllr, s, true, flags & LDPC_F_SPLIT));
-            HIP_TRY(timed(d, LDPC_K_COUNT, s, [&] {
-                return ldpc::launch_count(G, st, d->counters + (size_t)p * LDPC_MC_NCOUNT, s);
-            }));
+        if (int rc = ensure_pbits(d, G)) return rc;
+        for (int p = 0; p < n_points; ++p) {
+            for (int64_t start = 0; start < frames_per_point; start += cap) {
+                const int cnt = (int)std::min<int64_t>(cap, frames_per_point - start);
+                state_bind(d, (cnt + kTile - 1) / kTile, cnt);
+                HIP_TRY(ldpc::launch_reset(G, d->st, s));
+                const DevState st = d->st;
+                HIP_TRY(timed(d, LDPC_K_GEN, s,
+                              [&] { return ldpc::launch_frames(G, st, phys_tile(d), seed, p, sigmas[p], frame0 + start,
+                                                               ldpc::kFramesCh, nullptr, s); }));
+                if (int rc = run_iterations(d, G, st, max_iter, nllr, s, true, flags & LDPC_F_SPLIT)) return rc;
+                HIP_TRY(timed(d, LDPC_K_COUNT, s, [&] {
+                    return ldpc::launch_count(G, st, d->counters + (size_t)p * LDPC_MC_NCOUNT, s);
+                }));
+            }
         }
-    }
     }
     std::vector<unsigned long long> h(need);
     HIP_TRY(hipMemcpyAsync(h.data(), d->counters, sizeof(unsigned long long) * need, hipMemcpyDeviceToHost, s));

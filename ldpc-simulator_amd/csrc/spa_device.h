@@ -102,9 +102,9 @@ hipError_t launch_tile(const DevGraph &g, const DevState &st, int max_iter, bool
 // Streaming Monte-Carlo through the tile-resident decoder (one launch per SNR
 // point; LDPC_TILE_STREAM=0 keeps the split CN/VN/refill loop).
 bool use_tile_stream(const DevGraph &g);
-// handoff > 0 (sub-tile decoder only): the kernel stops once the supply is
-// out and at most `handoff` frames still run, leaving them as split-path
-// slot state (done / iters / fresh; E, L, ch, ubits in place)
+// handoff > 0 (the 16- and 8-frame sub-tile decoders): the kernel stops once
+// the supply is out and at most `handoff` frames still run, leaving them as
+// split-path slot state (done / iters / fresh; E, L, ch, ubits in place)
 hipError_t launch_tile_stream(const DevGraph &g, const DevState &st, int max_iter, bool nllr, uint64_t seed,
                               int snr_point, double sigma, int64_t frame0, int64_t total, unsigned long long *next,
                               unsigned long long *ctr, int64_t handoff, hipStream_t s);
@@ -113,6 +113,11 @@ hipError_t launch_tile_stream(const DevGraph &g, const DevState &st, int max_ite
 bool tile8_applies(const DevGraph &g);
 size_t tile8_lds_bytes(const DevGraph &g);
 hipError_t launch_tile8(const DevGraph &g, const DevState &st, int max_iter, bool nllr, hipStream_t s);
+// its streaming Monte-Carlo form (one persistent launch per SNR point, handoff as launch_tile_stream)
+size_t tile8_stream_lds_bytes(const DevGraph &g);
+hipError_t launch_tile8_stream(const DevGraph &g, const DevState &st, int max_iter, bool nllr, uint64_t seed,
+                               int snr_point, double sigma, int64_t frame0, int64_t total, unsigned long long *next,
+                               unsigned long long *ctr, int64_t handoff, hipStream_t s);
 size_t tile64_lds_bytes(const DevGraph &g);  // tile_kernel (64 frames per workgroup), 0 if it does not apply
 int sub_frames(const DevGraph &g);
 size_t sub_lds_bytes(const DevGraph &g);

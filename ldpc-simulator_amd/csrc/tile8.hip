@@ -679,6 +679,12 @@ __global__ __launch_bounds__(64 * kW8, 1) void tile8_kernel(DevGraph g, DevState
     }
     __syncthreads();
     if (!st.tile_active[tile]) return;
+    {  // a sub-tile with no live frame (a ragged batch's last tile) has nothing to do
+        int any = 0;
+#pragma unroll
+        for (int f = 0; f < kF8; ++f) any |= livel[f];
+        if (!any) return;  // block-uniform: LDS after the barrier
+    }
 
     T8Ctx<K> c;
     t8_setup<K, LA>(c, lds, ly, g, st, tile, sub, col_idx, row_ptr, ac);
@@ -748,6 +754,172 @@ __global__ __launch_bounds__(64 * kW8, 1) void tile8_kernel(DevGraph g, DevState
 #endif
 }
 
+// Streaming Monte-Carlo on 8-frame sub-tiles (tile_sub.hip's
+// tile_sub_stream_kernel at 8 frames per workgroup): every frame slot is at
+// its own iteration; after each pass a slot whose frame stopped adds that
+// frame's counters (count_kernel's definitions, main.py:130-138) and takes the
+// next frame index from one device counter; the whole workgroup generates the
+// new frames in place (frame_source.h gen_slots: ch and L = ch, so the frame's
+// next pass forms M = L - 0, its iteration 0 -- the `fresh` flag of P1, and
+// L_A = ch in LDS for the L_A variant).  Each frame decodes exactly as in the
+// static schedule, so the counters are identical.  With handoff > 0 the
+// workgroup stops once the supply is out and at most `handoff` frames still
+// run anywhere, leaving its slots in the split path's terms (done / iters /
+// fresh; E in 8-frame blocks, L, ch and u bits in place) for the
+// column-parallel tail (ldpc_api.cpp mc_stream_point).  Reference: the
+// per-frame loop of main.py:295-342 over spa_decoder.py:63-280.
+template <int K, bool LA, int D>
+__global__ __launch_bounds__(64 * kW8, 1) void tile8_stream_kernel(
+    DevGraph g, DevState st, int max_iter, int nllr, const int *__restrict__ col_idx,
+    const int *__restrict__ row_ptr, AtanhCoef ac, uint64_t seed, int snr_point, double sigma, int64_t frame0,
+    int64_t total, unsigned long long *next, unsigned long long *ctr, int64_t handoff) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+    __shared__ long long gidx[kF8];  // refill: slot f's new frame index (< 0: none)
+    __shared__ int nref;             // refill: some slot took a frame this pass
+    const T8Layout ly = t8_layout(g.k, g.m, K, LA, D + 1);
+    double *S = (double *)(lds + ly.S);
+    double *LAl = LA ? (double *)(lds + ly.LA) : nullptr;
+    uint32_t *zb = (uint32_t *)(lds + ly.zb);
+    uint32_t *ib = (uint32_t *)(lds + ly.ib);
+    int *bad = (int *)(lds + ly.lane_i);
+    int *cntl = bad + kF8;
+    int *livel = cntl + kF8;
+    int *itl = livel + kF8;
+    int *freshl = itl + kF8;
+    int *flags = (int *)(lds + ly.flags);
+    const int kw = (g.k + 31) >> 5, mw = (g.m + 31) >> 5;
+    const int tile = blockIdx.x / kQ8, sub = blockIdx.x % kQ8;
+    if (tile >= st.ntiles) return;  // block-uniform
+
+    fill_math_lds(*(MathLds *)(lds + ly.math));
+    for (int i = threadIdx.x; i < g.k * kF8; i += blockDim.x) S[i] = 0.0;
+    for (int i = threadIdx.x; i < (kw + mw) * kF8; i += blockDim.x) zb[i] = 0u;
+    if (threadIdx.x < 5 * kF8) bad[threadIdx.x] = 0;  // bad, cnt, live, it, fresh
+    if (threadIdx.x < 2 * kSR8) flags[threadIdx.x] = -1;
+    if (threadIdx.x >= 2 * kSR8 && threadIdx.x < 2 * kSR8 + 2 + kW8) flags[threadIdx.x] = 0;
+    const int lane = threadIdx.x & 63;
+    const bool w0 = (threadIdx.x >> 6) == 0;        // hardware wavefront 0 runs the refill and the exits
+    const bool slot_lane = threadIdx.x < kF8;       // the lane that owns frame slot f = lane
+    bool want = slot_lane;
+    const __amdgpu_buffer_rsrc_t rC = t8_rsrc(st.ch + (size_t)tile * g.n * kTile, (size_t)g.n * kTile * sizeof(double));
+    const __amdgpu_buffer_rsrc_t rL = t8_rsrc(st.L + (size_t)tile * g.n * kTile, (size_t)g.n * kTile * sizeof(double));
+
+    T8Ctx<K> c;
+    t8_setup<K, LA>(c, lds, ly, g, st, tile, sub, col_idx, row_ptr, ac);
+    c.R = D + 1;
+    c.idwave = D >= 3 ? 0 : kW8 - 1;  // as tile8_kernel
+    const int m = g.m;
+    const uint32_t *Ut = st.ubits + (size_t)tile * kw * kTile + sub * kF8 + lane;  // slot lanes only
+
+    for (int pass = 0;; ++pass) {
+        __syncthreads();  // the previous pass's exits (or the set-up) are visible
+        if (w0) {  // refill: slots without a frame take the next indices
+            int stop = 0;
+            if (handoff > 0 && lane == 0) {
+                const long long nx = (long long)__hip_atomic_load(next, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                const long long fin = (long long)__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                stop = nx >= total && total - fin <= handoff ? 1 : 0;
+            }
+            stop = uniform(stop);
+            if (stop) want = false;
+            const unsigned long long w = __ballot(want);
+            bool have = false;
+            if (w != 0ull) {
+                const int first = __ffsll((long long)w) - 1;
+                unsigned long long base = 0ull;
+                if (lane == first) base = atomicAdd(next, (unsigned long long)__popcll(w));
+                base = __shfl(base, first);
+                const unsigned long long below = lane ? (w & (~0ull >> (64 - lane))) : 0ull;
+                const int64_t idx = (int64_t)(base + (unsigned long long)__popcll(below));
+                have = want && idx < total;
+                if (slot_lane) gidx[lane] = have ? (long long)(frame0 + idx) : -1ll;
+                if (want) {
+                    livel[lane] = have ? 1 : 0;
+                    freshl[lane] = have ? 1 : 0;
+                    itl[lane] = 0;
+                }
+            } else if (slot_lane) {
+                gidx[lane] = -1ll;
+            }
+            const bool gen = __ballot(have) != 0ull;
+            want = false;
+            const bool go = __ballot(slot_lane && livel[lane] != 0) != 0ull && !stop;
+            if (!go && slot_lane) {  // the slots' state, in the split path's terms
+                const int fr = tile * kTile + sub * kF8 + lane;
+                st.done[fr] = livel[lane] != 0 ? 0 : 1;
+                st.iters[fr] = itl[lane];
+                st.fresh[fr] = freshl[lane];
+                st.refill[fr] = 0;
+            }
+            if (lane == 0) {
+                flags[2 * kSR8 + 1] = go ? 1 : 0;
+                nref = go && gen ? 1 : 0;
+            }
+        }
+        __syncthreads();
+        if (!flags[2 * kSR8 + 1]) break;  // supply exhausted (or handed off), every slot drained
+        if (nref) {  // the new frames, generated by the whole workgroup (u bits staged in zb)
+            gen_slots<kF8>(g, st, tile, sub * kF8, gidx, zb, seed, snr_point, sigma);
+            if constexpr (LA) {  // a new frame's first pass gathers L = ch
+                for (int e = threadIdx.x; e < g.k * kF8; e += blockDim.x)
+                    if (gidx[e & 7] >= 0)
+                        LAl[e] = t8_ld(rC, ((uint32_t)(e >> 3) << 9) + (uint32_t)(sub * kF8 + (e & 7)) * 8u);
+            }
+            __syncthreads();
+        }
+        c.live = livel[c.f] != 0;
+        c.fresh = freshl[c.f] != 0;
+        c.first = false;
+        c.ep0 = t8_epoch0(pass, m);
+        t8_rows<K, LA, D>(c);
+        __syncthreads();  // every P3 done: S complete, identity bits set
+        if (threadIdx.x < kW8) c.p3row[threadIdx.x] = 0;
+        t8_vn<LA>(g, S, LAl, zb, cntl, livel, rL, rC, sub, false, true, freshl, nllr);
+        __syncthreads();
+        t8_syndrome(g, zb, ib, bad);
+        __syncthreads();
+        if (w0) {  // per-slot exits and counters (vn_kernel's stream variant)
+            unsigned long long cv[7] = {0, 0, 0, 0, 0, 0, 0};
+            bool fin = false;
+            if (slot_lane && livel[lane] != 0) {
+                const int it = itl[lane];
+                const bool ok = bad[lane] == 0;  // Result.OK at this iteration (:231-241)
+                fin = ok || it == max_iter - 1;  // else DATA_TRANSFER_NOT_OK (:244-253)
+                if (fin) {
+                    int err = 0;
+                    if (!ok)  // main.py:130-138: u vs z^1 of a failed frame
+                        for (int w = 0; w < kw; ++w) err += __builtin_popcount(Ut[w * kTile] ^ zb[w * kF8 + lane]);
+                    cv[0] = 1;
+                    cv[1] = ok ? 0 : 1;
+                    cv[2] = (unsigned long long)err;
+                    cv[3] = ok ? (unsigned long long)it : 0;
+                    cv[4] = ok ? 1 : 0;
+                    cv[5] = nllr ? (unsigned long long)cntl[lane] : 0;
+                    cv[6] = (unsigned long long)(it + 1);
+                    livel[lane] = 0;
+                    want = true;
+                } else {
+                    itl[lane] = it + 1;
+                }
+                freshl[lane] = 0;
+            }
+            if (__ballot(fin) != 0ull) {
+#pragma unroll
+                for (int i = 0; i < 7; ++i) {
+                    const unsigned long long sm = wave_sum(cv[i]);
+                    if (lane == 0 && sm) atomicAdd(&ctr[i], sm);
+                }
+            }
+            if (slot_lane) {
+                bad[lane] = 0;
+                cntl[lane] = 0;
+            }
+        }
+        __syncthreads();  // wave 0 has read zb (error bits) before it is cleared
+        for (int i = threadIdx.x; i < (kw + mw) * kF8; i += blockDim.x) zb[i] = 0u;
+    }
+}
+
 // Variants: (K, L_A in LDS, pipeline depth D).  wimax_2304_0.5: (5, yes, 3);
 // the r3/4 codes: (8, no, 2) -- 8 slots per lane leave no registers for a
 // third row of t.
@@ -790,6 +962,36 @@ size_t tile8_lds_bytes(const DevGraph &g) {
         case 16: return t8_lds_bytes_k<8, false, kD8>(g);
         default: return 0;
     }
+}
+
+// tile8_stream_kernel's LDS: the static decoder's + gidx[8], nref (static __shared__)
+size_t tile8_stream_lds_bytes(const DevGraph &g) {
+    const size_t b = tile8_lds_bytes(g);
+    return b && b + kF8 * sizeof(long long) + 16 <= kLds8Max ? b : 0;
+}
+
+hipError_t launch_tile8_stream(const DevGraph &g, const DevState &st, int max_iter, bool nllr, uint64_t seed,
+                               int snr_point, double sigma, int64_t frame0, int64_t total, unsigned long long *next,
+                               unsigned long long *ctr, int64_t handoff, hipStream_t s) {
+    const size_t lds = tile8_lds_bytes(g);
+    if (!tile8_stream_lds_bytes(g) || g.ef != kF8 || !g.a_packed || !st.ubits || st.ntiles > st.nslots)
+        return hipErrorInvalidValue;
+    const dim3 grid(st.ntiles * kQ8), block(64 * kW8);
+    switch (t8_variant(g)) {
+        case 11:
+            tile8_stream_kernel<5, true, kD5><<<grid, block, lds, s>>>(g, st, max_iter, nllr ? 1 : 0, g.col_idx,
+                                                                      g.row_ptr, kAtanhCoef, seed, snr_point, sigma,
+                                                                      frame0, total, next, ctr, handoff);
+            break;
+        case 16:
+            tile8_stream_kernel<8, false, kD8><<<grid, block, lds, s>>>(g, st, max_iter, nllr ? 1 : 0, g.col_idx,
+                                                                       g.row_ptr, kAtanhCoef, seed, snr_point, sigma,
+                                                                       frame0, total, next, ctr, handoff);
+            break;
+        default:
+            return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
 }
 
 hipError_t launch_tile8(const DevGraph &g, const DevState &st, int max_iter, bool nllr, hipStream_t s) {

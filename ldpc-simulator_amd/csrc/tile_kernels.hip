@@ -705,8 +705,8 @@ bool use_tile(const DevGraph &g) {
 }
 
 // Streaming Monte-Carlo in one persistent launch per SNR point: tile_stream_kernel
-// (64 frames per workgroup) or tile_sub_stream_kernel (16-frame sub-tiles,
-// wimax_2304_0.5).  LDPC_TILE_STREAM=0 falls back to the separate launches.
+// (64 frames per workgroup), tile_sub_stream_kernel (16-frame sub-tiles,
+// wimax_2304_0.5) or tile8_stream_kernel (8-frame sub-tiles: the r3/4 codes).  LDPC_TILE_STREAM=0 falls back to the separate launches.
 static bool sub16(const DevGraph &g) { return sub_enabled(g) && sub_frames(g) == 16; }
 bool use_tile_stream(const DevGraph &g) {
     const char *e = getenv("LDPC_TILE_STREAM");
@@ -715,7 +715,7 @@ bool use_tile_stream(const DevGraph &g) {
     // + the kernel's static per-lane state (itl, freshl: 2 x 64 ints; gidx: 64
     // frame indices; the refill flag)
     if (lds) return lds + 2 * kTile * sizeof(int) + kTile * sizeof(long long) + 16 <= kTileLdsMax;
-    if (g.ef == 8) return false;  // tile8.hip: static launches; streaming runs the split loop
+    if (g.ef == 8) return tile8_stream_lds_bytes(g) > 0;  // tile8.hip: tile8_stream_kernel
     return sub16(g);
 }
 
@@ -723,6 +723,9 @@ hipError_t launch_tile_stream(const DevGraph &g, const DevState &st, int max_ite
                               int snr_point, double sigma, int64_t frame0, int64_t total, unsigned long long *next,
                               unsigned long long *ctr, int64_t handoff, hipStream_t s) {
     const size_t lds = tile64_lds_bytes(g);
+    if (!lds && g.ef == 8)
+        return launch_tile8_stream(g, st, max_iter, nllr, seed, snr_point, sigma, frame0, total, next, ctr, handoff,
+                                   s);
     if (!lds && sub16(g))
         return launch_tile_sub_stream(g, st, max_iter, nllr, seed, snr_point, sigma, frame0, total, next, ctr,
                                       handoff, s);

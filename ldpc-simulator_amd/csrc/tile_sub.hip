@@ -645,6 +645,12 @@ __global__ __launch_bounds__(64 * kSW, 1) void tile_sub_kernel(DevGraph g, DevSt
     if (wave == 0 && j == 0) livel[f] = st.done[fr] == 0 ? 1 : 0;
     __syncthreads();
     if (!st.tile_active[tile]) return;
+    {  // a sub-tile with no live frame (a ragged batch's last tile) has nothing to do
+        int any = 0;
+#pragma unroll
+        for (int ff = 0; ff < F; ++ff) any |= livel[ff];
+        if (!any) return;  // block-uniform: LDS after the barrier
+    }
 
     SubCtx<Q> c;
     c.col_idx = col_idx;

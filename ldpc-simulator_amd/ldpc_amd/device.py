@@ -246,7 +246,8 @@ class Decoder:
             out.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)), None))
         return out
 
-    KINDS = ("cn", "vn", "generate", "count", "phys", "phys_cn", "phys_vn", "tile")
+    KINDS = ("cn", "vn", "generate", "count", "phys", "phys_cn", "phys_vn", "tile", "cn_edge", "vn_edge",
+             "vn_cols")
 
     def profile(self, enable=True):
         check("ldpc_profile_enable", _lib.gpu().ldpc_profile_enable(self._h, 1 if enable else 0))

@@ -81,20 +81,21 @@ def test_edge_path_matches_reference_golden(gpu_available):
 
 
 def test_edge_path_is_the_one_launched(gpu_available, monkeypatch):
-    """A one-frame call runs cn_edge_kernel (no tile launch); 9 frames do not."""
-    from ldpc_amd import _lib
+    """A one-frame call and a 9-frame call (both <= LDPC_EDGE_FRAMES, 32 for
+    the 2304 codes) run cn_edge_kernel + vn_edge_kernel and nothing else
+    (the exact cut-overs: tests/test_gpu_decoders.py test_cutover_thresholds)."""
     dec = _decoder("wimax_2304_0.5", 64)
     llr = _random_llr(hstd_for("wimax_2304_0.5"), 9, 2.0, seed=5)
-    dec.profile(True)
-    dec.decode(llr[:1], 4)
-    p = dec.profile_read()
-    assert p["tile"][1] == 0 and p["cn"][1] > 0, p
-    dec.decode(llr, 4)
-    dec.profile(False)
-    assert _lib.lib().ldpc_abi_version() >= 3
+    for B in (1, 9):
+        dec.profile(True)
+        dec.decode(llr[:B], 4)
+        p = dec.profile_read()
+        dec.profile(False)
+        assert p["cn_edge"][1] == 4 and p["vn_edge"][1] == 4, p
+        assert p["tile"][1] == 0 and p["cn"][1] == 0 and p["vn"][1] == 0 and p["vn_cols"][1] == 0, p
     # both calls agree with the frame-per-lane path on their frames
     monkeypatch.setenv("LDPC_EDGE_FRAMES", "0")
-    a = dec.decode(llr[:1], 4, post=True)
+    a = dec.decode(llr, 4, post=True)
     monkeypatch.delenv("LDPC_EDGE_FRAMES")
-    b = dec.decode(llr[:1], 4, post=True)
+    b = dec.decode(llr, 4, post=True)
     np.testing.assert_array_equal(a.post, b.post)

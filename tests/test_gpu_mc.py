@@ -144,6 +144,9 @@ def test_stream_zero_frames(gpu_available):
     ("wimax_576_0.5", 4096, 70, 8, (0.5,)),         # far fewer frames than slots (idle workgroups)
     ("wimax_2304_0.5", 256, 700, 12, (1.0, 3.0)),   # 16-frame sub-tiles (tile_sub_stream_kernel)
     ("wimax_2304_0.5", 64, 150, 1, (2.0,)),         # sub-tiles, max_iter 1
+    ("wimax_2304_0.75A", 256, 700, 12, (2.0, 3.5)),  # 8-frame sub-tiles (tile8_stream_kernel, K = 8)
+    ("wimax_2304_0.75B", 64, 150, 1, (2.0,)),        # tile8 streaming, max_iter 1
+    ("wimax_2304_0.75A", 4096, 70, 8, (3.0,)),       # far fewer frames than slots
 ])
 def test_tile_stream_equals_split_stream(gpu_available, code, cap, frames, T, snrs, monkeypatch):
     monkeypatch.setenv("LDPC_HANDOFF", "0")  # the whole point in the tile kernel (hand-off: next test)
@@ -195,13 +198,15 @@ def test_fit_slots_caps_the_workspace(gpu_available):
     assert ctr[0, 0] == 3 * slots + 5
 
 
-@pytest.mark.parametrize("handoff", ["256", "20"])
-def test_stream_handoff_keeps_counters(gpu_available, monkeypatch, handoff):
-    """The streaming sub-tile kernel hands its last running frames to the split
-    path's column-parallel tail (launch_vn_tail) once the supply is out: the
-    counters equal the sub-tile kernel draining alone, the static schedule and
-    the split stream with the per-tile vn_kernel."""
-    code, cap, frames, T = "wimax_2304_0.5", 256, 1500, 20
+@pytest.mark.parametrize("code,handoff", [("wimax_2304_0.5", "256"), ("wimax_2304_0.5", "20"),
+                                          ("wimax_2304_0.75A", "256"), ("wimax_2304_0.75A", "20")])
+def test_stream_handoff_keeps_counters(gpu_available, monkeypatch, code, handoff):
+    """The streaming sub-tile kernels (16-frame tile_sub_stream_kernel, 8-frame
+    tile8_stream_kernel) hand their last running frames to the split path's
+    column-parallel tail (launch_vn_tail) once the supply is out: the counters
+    equal the sub-tile kernel draining alone, the static schedule and the
+    split stream with the per-tile vn_kernel."""
+    cap, frames, T = 256, 1500, 20
     dec = _decoder(code, cap)
     sig = [oracle.sigma_for_snr(s) for s in (2.5, 3.0)]
     monkeypatch.setenv("LDPC_HANDOFF", handoff)
@@ -220,3 +225,49 @@ def test_stream_handoff_keeps_counters(gpu_available, monkeypatch, handoff):
     for x in (b, c, d, e):
         np.testing.assert_array_equal(a, x)
     assert (a[:, 0] == frames).all()
+
+
+def test_tile8_stream_matches_oracle_config4(gpu_available):
+    """Config 4's decoder: the 8-frame streaming kernel on wimax_2304_0.75A at
+    T=50 (the bench's config4 sweep runs exactly this call), frames through 64
+    slots so that every slot decodes several; counters == the oracle's
+    main.py counters on the very frames the device generated, per point."""
+    code, cap, frames, T = "wimax_2304_0.75A", 64, 96, 50
+    H = hstd_for(code)
+    k = H.shape[1] - H.shape[0]
+    snrs = (2.5, 3.0, 4.0)
+    sig = [oracle.sigma_for_snr(s) for s in snrs]
+    dec = _decoder(code, cap)
+    dec.profile(True)
+    ctr = dec.mc_run(SEED, sig, frames, 5000, T, nllr=True)
+    p = dec.profile_read()
+    dec.profile(False)
+    assert p["tile"][1] == len(snrs), p  # one tile8_stream_kernel launch per point
+    gen = _decoder(code, frames)
+    for i, sg in enumerate(sig):
+        u, llr = gen.generate(SEED, i, sg, 5000, frames)
+        o = oracle.spa_decode(H, llr, T, nllr=True)
+        want = oracle.main_counters(u, o["z"], o["status"], o["conv"],
+                                    nllr_cnt=np.rint(o["nllr"] * k).astype(np.int64), iters=o["iters"])
+        np.testing.assert_array_equal(ctr[i], want, err_msg=f"{snrs[i]} dB")
+
+
+def test_tile8_stream_r12_equals_static(gpu_available, monkeypatch):
+    """tile8's L_A-in-LDS variant (wimax_2304_0.5 with LDPC_TILE8=1): the
+    streaming kernel (L_A reloaded from ch for refilled slots) == its static
+    schedule == the default graph's tile_sub decoders."""
+    from ldpc_amd.device import Decoder, Graph
+    code, cap, frames, T = "wimax_2304_0.5", 128, 400, 15
+    sig = [oracle.sigma_for_snr(s) for s in (1.5, 3.0)]
+    monkeypatch.setenv("LDPC_TILE8", "1")
+    g8 = Graph(hstd_for(code))
+    monkeypatch.delenv("LDPC_TILE8")
+    d8 = Decoder(g8, cap)
+    monkeypatch.setenv("LDPC_HANDOFF", "0")
+    a = d8.mc_run(SEED, sig, frames, 9, T, nllr=True)
+    monkeypatch.delenv("LDPC_HANDOFF")
+    b = d8.mc_run(SEED, sig, frames, 9, T, nllr=True)  # with the hand-off to the split tail
+    c = d8.mc_run(SEED, sig, frames, 9, T, nllr=True, static=True)
+    d = _decoder(code, cap).mc_run(SEED, sig, frames, 9, T, nllr=True)
+    for x in (b, c, d):
+        np.testing.assert_array_equal(a, x)

@@ -62,8 +62,12 @@ def _random_llr(H, B, snr_db, seed):
     ("wimax_576_0.5", 200, 8, 1.5),
     ("wimax_576_0.5", 130, 20, 2.5),
     ("wimax_2304_0.75A", 64, 3, 3.0),
-    # the north-star code at config 3's point: 50 saturating iterations at 1 dB
-    # (where the GPU's atanh and the reference's SVML arctanh could part at the ulp)
+    # the north-star code at 50 saturating iterations at 1 dB (where the GPU's
+    # atanh and the reference's SVML arctanh could part at the ulp).  64 and 70
+    # frames are 1-2 tiles: the default route is the split CN + column-parallel
+    # VN (ldpc_api.cpp small_batch_cols), NOT the headline's tile_sub_kernel --
+    # that one meets the oracle in tests/test_gpu_config3.py (the bench's exact
+    # call) and every decoder meets the golden vectors in test_gpu_decoders.py
     ("wimax_2304_0.5", 64, 50, 1.0),
     ("wimax_2304_0.5", 70, 50, 2.0),   # ragged: one full and one partial 64-frame tile
 ])

@@ -1,18 +1,20 @@
 #!/bin/bash
-# Physical mode: rocprofv3 trace + VALU counters of
-# phys_reg_kernel (its state lives in LDS: the bound is VALU issue, not HBM),
-# then the split streaming path's drain tail at 3 dB (config 3, SURVEY §8 d).
-# usage: tools/profile_phys.sh TAG ; outputs under gpurun_out/TAG
-set -e
-TAG=${1:-prof_phys}
+# Physical mode: per SNR point, a rocprofv3 kernel trace and
+# one PMC pass of SQ counters over `bench.py --mode physical` -- the VALU
+# instructions per frame-iteration of phys_reg_kernel (its state lives in LDS:
+# the bound is VALU issue, not HBM) that bench.py's physical roofline prices
+# against (committed_valu: code, kernel and SNR must match).
+# usage: tools/profile_phys.sh TAG [SNR ...]   (default SNRs: 1.0 -2.5)
+# then:  python3 tools/summarize_phys_profile.py gpurun_out/TAG profiles/TAG
+set -o pipefail
+TAG=${1:-prof_phys}; shift
+SNRS=${*:-1.0 -2.5}
 export TMPDIR=/tmp
 OUT=gpurun_out/$TAG
 mkdir -p $OUT
-P="--mode physical --snr 0.0 --frames 65536 --steps 2 --warmup 1 --cpu-seconds 0 --extra-snr="
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/phys_trace -o run -- python3 bench.py $P > $OUT/phys_trace.log 2>&1
-timeout -s KILL 300 rocprofv3 --pmc SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_LDS SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY --output-format csv -d $OUT/phys_sq -o run -- python3 bench.py $P > $OUT/phys_sq.log 2>&1
-timeout -s KILL 300 rocprofv3 --pmc GRBM_GUI_ACTIVE GRBM_COUNT --output-format csv -d $OUT/phys_grbm -o run -- python3 bench.py $P > $OUT/phys_grbm.log 2>&1
-S="--snr 3.0 --frames 32768 --chunk 16384 --steps 1 --warmup 1 --cpu-seconds 0 --extra-snr= --schedule stream"
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/tail_trace -o run -- python3 bench.py $S > $OUT/tail_trace.log 2>&1
-python3 bench.py $S > $OUT/tail_bench.json 2>/dev/null
+for X in $SNRS; do
+    P="--mode physical --snr $X --frames 262144 --steps 2 --warmup 1 --cpu-seconds 0 --extra-snr= --point-snr= --config4-snr= --dropin-calls 0"
+    timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace_$X -o run -- python3 bench.py $P > $OUT/trace_$X.log 2>&1 || exit 1
+    timeout -s KILL 300 rocprofv3 --pmc SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_LDS SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY --output-format csv -d $OUT/sq_$X -o run -- python3 bench.py $P > $OUT/sq_$X.log 2>&1 || exit 1
+done
 echo done
