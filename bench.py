@@ -17,9 +17,12 @@ timed region, one step each at --extra-snr points (default 2.0 and 3.0 dB) is
 timed and reported under "snr_points" (scope "step"), then --point-snr (default
 3.0 dB) as ONE whole config-3 point of 262,144 frames per GPU streamed in one
 run (scope "point": the streaming tail is paid once per point, as main.py pays
-it), and a few steps of the physical mode
-(the north-star's absolute cw/s target, NOT the
-reference's arithmetic) under "physical".
+it), a few steps of the physical mode (the
+north-star's absolute cw/s target, NOT the reference's arithmetic) under
+"physical" at the headline's SNR and at a waterfall point, and BASELINE
+config 4 under "config4": wimax_2304_0.75A over main.py's 1.0:0.5:4.0 dB grid,
+32,768 frames per GPU per point (one GPU's shard of 262,144), each point one
+streaming run of the 8-frame sub-tile decoder, plus one static tile8 step.
 
 Launch: under torch.distributed.run (RANK / WORLD_SIZE set) every process is
 one rank.  `bench.py --gpus N` (N > 1) with no launcher around it starts its
@@ -425,13 +428,13 @@ def physical_extra(args, edd, graph, local, world, rank, dist, k):
 
 
 def snr_grid(spec):
-    """main.py's SNR grid (main.py:193,206-209): steps = ceil((end - start) / step) + 1,
-    the last point clamped to end.  spec 'start:step:end' or a comma list."""
+    """'start:step:end' -> main.py's SNR grid (ldpc_amd.montecarlo.snr_grid,
+    main.py:193,206-209), or a comma list."""
     if ":" not in spec:
         return [float(v) for v in spec.split(",") if v.strip()]
+    from ldpc_amd.montecarlo import snr_grid as grid
     a, st, b = (float(v) for v in spec.split(":"))
-    n = int(math.ceil((b - a) / st)) + 1
-    return [round(min(a + i * st, b), 10) for i in range(n)]
+    return [float(x) for x in grid(a, b, st)]
 
 
 def config4_extra(args, local, world, rank, dist):

@@ -48,6 +48,7 @@ struct ldpc_graph {
     std::vector<int> h_row_ptr, h_col_idx;
     int *d_ints = nullptr;       // one allocation for all index arrays
     uint32_t *d_apack = nullptr;  // bit-packed A (std_form graphs only)
+    uint16_t *d_col16 = nullptr;  // col_idx as uint16 (n <= 65535)
 };
 
 struct ldpc_decoder {
@@ -76,6 +77,12 @@ struct ldpc_decoder {
     uint32_t *tzb = nullptr;  // streaming tail VN: z^1 bits [cap_tiles][ceil(n/32)][64], zero between uses
     int *tcnt = nullptr;      // streaming tail VN: normalized-LLR counts [cap_tiles*64], zero between uses
     int *tbad = nullptr;      // few-frame decode path: row-parity flags [cap_tiles*64], zero between uses
+    // streaming supply order (frame_order.hip), grow-only: keys 2 x ord_cap, vals / order ord_cap each
+    uint32_t *ord_keys = nullptr;
+    int *ord_vals = nullptr, *ord = nullptr;
+    int64_t ord_cap = 0;
+    void *ord_tmp = nullptr;
+    size_t ord_tmp_bytes = 0;
     DevState st{};
     // profiling (ldpc_profile_*)
     bool prof = false;
@@ -225,6 +232,7 @@ void state_bind(ldpc_decoder *d, int ntiles, int count) {
     s.nllr_cnt = d->ints + 4 * cap;
     s.fresh = d->ints + 5 * cap;
     s.refill = d->ints + 6 * cap;
+    s.order = nullptr;
     s.tile_active = d->ints + 7 * cap;
     s.ubits = d->ubits;
     s.nllr_hist = nullptr;
@@ -536,11 +544,19 @@ int ldpc_graph_create(int32_t m, int32_t n, const int32_t *row_ptr, const int32_
             e = hipMemcpy(g->d_apack, ap.data(), sizeof(uint32_t) * ap.size(), hipMemcpyHostToDevice);
         G.a_packed = g->d_apack;
     }
+    if (e == hipSuccess && n <= 65535) {
+        std::vector<uint16_t> c16(col_idx, col_idx + nnz);
+        if (dev_alloc(&g->d_col16, c16.size())) e = hipErrorOutOfMemory;
+        if (e == hipSuccess)
+            e = hipMemcpy(g->d_col16, c16.data(), sizeof(uint16_t) * c16.size(), hipMemcpyHostToDevice);
+        G.col16 = g->d_col16;
+    }
     // the WiMAX 2304 codes run the 8-frame sub-tile decoder: E in 8-frame blocks
     if (e == hipSuccess && !ldpc::tile64_lds_bytes(G) && ldpc::tile8_applies(G)) G.ef = 8;
     if (e != hipSuccess) {
         (void)hipFree(g->d_ints);
         (void)hipFree(g->d_apack);
+        (void)hipFree(g->d_col16);
         delete g;
         return ldpc_fail(LDPC_EDEVICE, "ldpc_graph_create: upload failed: %s", hipGetErrorString(e));
     }
@@ -553,6 +569,7 @@ int ldpc_graph_destroy(ldpc_graph *g) {
     DeviceGuard dg(g->device);
     (void)hipFree(g->d_ints);
     (void)hipFree(g->d_apack);
+    (void)hipFree(g->d_col16);
     delete g;
     return LDPC_OK;
 }
@@ -642,6 +659,10 @@ int ldpc_decoder_destroy(ldpc_decoder *d) {
     (void)hipFree(d->tzb);
     (void)hipFree(d->tcnt);
     (void)hipFree(d->tbad);
+    (void)hipFree(d->ord_keys);
+    (void)hipFree(d->ord_vals);
+    (void)hipFree(d->ord);
+    (void)hipFree(d->ord_tmp);
     (void)hipFree(d->hist);
     (void)hipFree(d->L);
     (void)hipFree(d->ch);
@@ -873,6 +894,40 @@ int64_t handoff_frames(int64_t slots, int fpw) {
     return std::min<int64_t>(slots, (int64_t)cus * fpw) * 3 / 5;
 }
 
+// Longest job first (frame_order.hip): the point's frames enter the slots in
+// descending syndrome weight of their channel hard decisions, so the frames
+// that will run to max_iter start while the slots are still being refilled
+// instead of forming a tail after the supply is out.  Counters are sums over
+// the point's frames, identical in any order.  LDPC_LPT=0: frame index order.
+bool lpt_enabled() {
+    const char *e = getenv("LDPC_LPT");
+    return !e || atoi(e) != 0;
+}
+int ensure_order(ldpc_decoder *d, int64_t total) {
+    if (d->ord_cap < total) {
+        (void)hipFree(d->ord_keys);
+        (void)hipFree(d->ord_vals);
+        (void)hipFree(d->ord);
+        d->ord_keys = nullptr;
+        d->ord_vals = d->ord = nullptr;
+        d->ord_cap = 0;
+        if (int rc = dev_alloc(&d->ord_keys, 2 * (size_t)total)) return rc;
+        if (int rc = dev_alloc(&d->ord_vals, (size_t)total)) return rc;
+        if (int rc = dev_alloc(&d->ord, (size_t)total)) return rc;
+        d->ord_cap = total;
+    }
+    const size_t tb = ldpc::frame_order_temp_bytes((int)total);
+    if (d->ord_tmp_bytes < tb) {
+        (void)hipFree(d->ord_tmp);
+        d->ord_tmp = nullptr;
+        d->ord_tmp_bytes = 0;
+        if (hipMalloc(&d->ord_tmp, tb) != hipSuccess)
+            return ldpc_fail(LDPC_ENOMEM, "hipMalloc(%zu bytes) failed (frame order scratch)", tb);
+        d->ord_tmp_bytes = tb;
+    }
+    return LDPC_OK;
+}
+
 // Streaming schedule of one SNR point: the decoder's cap frames are slots.  A
 // slot whose frame finishes (vn_kernel) is refilled with the next frame index
 // (refill_kernel), so no slot waits for the slowest frame of its tile or
@@ -883,7 +938,17 @@ int mc_stream_point(ldpc_decoder *d, uint64_t seed, int p, double sigma, int64_t
     if (total == 0) return LDPC_OK;
     const DevGraph &G = d->g->dg;
     const int ntiles = (int)std::min<int64_t>(d->cap_tiles, (total + kTile - 1) / kTile);
+    const int *order = nullptr;  // supply order (null: frame index order)
+    if (lpt_enabled() && total > 1 && total <= INT32_MAX && G.std_form && G.a_packed && G.m <= 65535) {
+        if (int rc = ensure_order(d, total)) return rc;
+        HIP_TRY(timed(d, LDPC_K_GEN, s, [&] {
+            return ldpc::launch_frame_order(G, seed, p, sigma, frame0, (int)total, d->ord_keys, d->ord_vals, d->ord,
+                                            d->ord_tmp, d->ord_tmp_bytes, s);
+        }));
+        order = d->ord;
+    }
     state_bind(d, ntiles, ntiles * kTile);
+    d->st.order = order;
     DevState st = d->st;
     unsigned long long *ctr = d->counters + (size_t)p * LDPC_MC_NCOUNT;
     unsigned long long *next = d->counters + d->counters_cap;
@@ -919,6 +984,7 @@ int mc_stream_point(ldpc_decoder *d, uint64_t seed, int p, double sigma, int64_t
         if (nt < cur) {
             HIP_TRY(ldpc::launch_compact(G, st, nt, cap, d->cpairs, s));
             state_bind(d, nt, nt * kTile);
+            d->st.order = order;
             st = d->st;
             cur = nt;
         } else {
@@ -975,6 +1041,7 @@ int mc_stream_point(ldpc_decoder *d, uint64_t seed, int p, double sigma, int64_t
             if (!d->cpairs && dev_alloc(&d->cpairs, 1 + 2 * (size_t)cap)) return LDPC_ENOMEM;
             HIP_TRY(ldpc::launch_compact(G, st, nt, cap, d->cpairs, s));
             state_bind(d, nt, nt * kTile);
+            d->st.order = order;
             st = d->st;
             cur = nt;
         }

@@ -43,6 +43,8 @@ struct DevGraph {
     const int *p3dep;          // [m][16] sub-tile S order: lo | hi << 8 (tile_sub.hip sub_p3)
     const int *p3dep8;         // [m][16] the same over each row's A edges (tile8.hip: identity excluded)
     int ef;                    // frames per E block (64, or 8 for tile8.hip's graphs): e_base
+    const uint16_t *col16;     // [nnz] col_idx as uint16 (n <= 65535; else null): the tile kernels'
+                               // index staging reads half the bytes (L2 footprint shared with the L gather)
 };
 
 // E layout inside a tile: the 64 frames in blocks of g.ef, each block
@@ -58,6 +60,8 @@ struct DevState {
     int *done, *conv, *status, *iters, *nllr_cnt;
     int *tile_active;
     int *fresh, *refill;     // streaming Monte-Carlo: lane holds a new frame / lane wants one
+    const int *order;        // streaming Monte-Carlo: local frame index of supply position i (frame_order.hip:
+                             // heaviest syndrome first), or null: frame index order
     int *rare_list;          // [ntiles*m] tile*m+row of rows left to cn_rare_kernel
     int *rare_count;         // [2] per iteration parity
     int *active_count;       // [max_iter] or null: vn_kernel adds the tiles still running after it
@@ -146,6 +150,16 @@ int edge_max_deg();
 hipError_t launch_cn_edge(const DevGraph &g, const DevState &st, int it, hipStream_t s);
 hipError_t launch_vn_edge_decode(const DevGraph &g, const DevState &st, int it, bool last, bool nllr, uint32_t *zb,
                                  int *cnt, int *gbad, hipStream_t s);
+// supply order of a streamed point (frame_order.hip): keys 2 x total uint32,
+// vals total int scratch, order total int out, temp frame_order_temp_bytes
+size_t frame_order_temp_bytes(int total);
+hipError_t launch_frame_order(const DevGraph &g, uint64_t seed, int snr_point, double sigma, int64_t frame0,
+                              int total, uint32_t *keys, int *vals, int *order, void *temp, size_t temp_bytes,
+                              hipStream_t s);
+// the global frame index of supply position idx of a point starting at frame0
+__device__ __forceinline__ long long supply_frame(const DevState &st, int64_t frame0, int64_t idx) {
+    return (long long)(frame0 + (st.order ? (int64_t)st.order[idx] : idx));
+}
 hipError_t launch_refill(const DevGraph &g, const DevState &st, uint64_t seed, int snr_point, double sigma,
                          int64_t frame0, int64_t total, unsigned long long *next, hipStream_t s);
 // streaming tail: move the frames running in tiles >= nt into finished slots

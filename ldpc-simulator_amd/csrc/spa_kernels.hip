@@ -766,7 +766,7 @@ __global__ __launch_bounds__(kRefillThreads) void refill_kernel(DevGraph g, DevS
             base = __shfl(base, __ffsll((long long)want) - 1);
             const int64_t idx = (int64_t)(base + (unsigned long long)__popcll(below));
             have = need && idx < total;
-            if (have) gi = (long long)(frame0 + idx);
+            if (have) gi = supply_frame(st, frame0, idx);
             if (need) {
                 st.refill[f] = 0;
                 st.done[f] = have ? 0 : 1;

@@ -161,6 +161,7 @@ __device__ __forceinline__ T8Chunk t8_chunk(const int *__restrict__ row_ptr, int
 template <int K>
 struct T8Ctx {
     const int *__restrict__ col_idx;
+    const uint16_t *__restrict__ col16;
     const int *__restrict__ row_ptr;
     const int *p3dep;
     // buffer resources (uniform) + per-lane byte offsets eo8 (E block: f * 8)
@@ -214,6 +215,10 @@ __device__ __forceinline__ int t8_stage_issue(const T8Ctx<K> &c, int q) {
     if (q >= c.m) return 0;
     const T8Chunk rc = t8_chunk(c.row_ptr, q, c.wave);
     const int L = threadIdx.x & 63;
+#ifndef LDPC_COL16
+#define LDPC_COL16 0
+#endif
+    if (LDPC_COL16) return rc.cnt > 0 ? (int)c.col16[rc.c0 + min(L, rc.cnt - 1)] : 0;
     return rc.cnt > 0 ? c.col_idx[rc.c0 + min(L, rc.cnt - 1)] : 0;
 }
 template <int K>
@@ -554,6 +559,7 @@ __device__ __forceinline__ void t8_setup(T8Ctx<K> &c, unsigned char *lds, const 
     int *flags = (int *)(lds + ly.flags);
     const int lane = threadIdx.x & 63;
     c.col_idx = col_idx;
+    c.col16 = g.col16;
     c.row_ptr = row_ptr;
     c.p3dep = g.p3dep8;
     c.wave = uniform(t8_wave(threadIdx.x >> 6));
@@ -832,7 +838,7 @@ __global__ __launch_bounds__(64 * kW8, 1) void tile8_stream_kernel(
                 const unsigned long long below = lane ? (w & (~0ull >> (64 - lane))) : 0ull;
                 const int64_t idx = (int64_t)(base + (unsigned long long)__popcll(below));
                 have = want && idx < total;
-                if (slot_lane) gidx[lane] = have ? (long long)(frame0 + idx) : -1ll;
+                if (slot_lane) gidx[lane] = have ? supply_frame(st, frame0, idx) : -1ll;
                 if (want) {
                     livel[lane] = have ? 1 : 0;
                     freshl[lane] = have ? 1 : 0;

@@ -473,7 +473,7 @@ __global__ __launch_bounds__(64 * kTW, 1) void tile_kernel(DevGraph g, DevState 
 // wave 0 of the streaming kernel: lanes with `want` take the next frame
 // indices (one wave-aggregated atomicAdd) into gidx; the whole workgroup then
 // generates them (frame_source.h gen_slots).  -> some lane took a frame.
-__device__ __forceinline__ bool tile_refill(int lane, bool want, int64_t frame0, int64_t total,
+__device__ __forceinline__ bool tile_refill(const DevState &st, int lane, bool want, int64_t frame0, int64_t total,
                                            unsigned long long *next, long long *gidx, int *livel, int *freshl,
                                            int *itl) {
     const unsigned long long w = __ballot(want);
@@ -484,7 +484,7 @@ __device__ __forceinline__ bool tile_refill(int lane, bool want, int64_t frame0,
     const unsigned long long below = lane ? (w & (~0ull >> (64 - lane))) : 0ull;
     const int64_t idx = (int64_t)(base + (unsigned long long)__popcll(below));
     const bool have = want && idx < total;
-    gidx[lane] = have ? (long long)(frame0 + idx) : -1ll;
+    gidx[lane] = have ? supply_frame(st, frame0, idx) : -1ll;
     if (want) {
         livel[lane] = have ? 1 : 0;
         freshl[lane] = have ? 1 : 0;
@@ -564,7 +564,7 @@ __global__ __launch_bounds__(64 * kTW, 1) void tile_stream_kernel(DevGraph g, De
         // cleared here)
         if (wave == 0) {
             bool gen = false;
-            if (__ballot(want) != 0ull) gen = tile_refill(lane, want, frame0, total, next, gidx, livel, freshl, itl);
+            if (__ballot(want) != 0ull) gen = tile_refill(st, lane, want, frame0, total, next, gidx, livel, freshl, itl);
             want = false;
             const unsigned long long any = __ballot(livel[lane] != 0);
             if (lane == 0) {

@@ -161,6 +161,7 @@ struct SubCtx {
     static constexpr int F = SubCfg<Q>::F;
     static constexpr int K = SubCfg<Q>::K;
     const int *__restrict__ col_idx;
+    const uint16_t *__restrict__ col16;
     const int *__restrict__ row_ptr;
     // per-lane bases: element (item) of this lane's frame at [item * 64]
     double *Eb;
@@ -212,8 +213,13 @@ template <int Q>
 __device__ __forceinline__ const double *sub_c(const SubCtx<Q> &c, int col) {
     return (const double *)(c.Cu + sub_off(c, col));
 }
+// LDPC_COL16 (A/B): stage the indices from the graph's uint16 copy
+#ifndef LDPC_COL16
+#define LDPC_COL16 0
+#endif
 template <int Q>
 __device__ __forceinline__ int sub_col(const SubCtx<Q> &c, int edge) {
+    if (LDPC_COL16) return *(const uint16_t *)((const char *)c.col16 + ((uint32_t)edge << 1));
     return *(const int *)((const char *)c.col_idx + ((uint32_t)edge << 2));
 }
 // This lane's piece of row r's staged column indices: slot i at [i].  The
@@ -654,6 +660,7 @@ __global__ __launch_bounds__(64 * kSW, 1) void tile_sub_kernel(DevGraph g, DevSt
 
     SubCtx<Q> c;
     c.col_idx = col_idx;
+    c.col16 = g.col16;
     c.row_ptr = row_ptr;
     const size_t lo = (size_t)sub * F + f;
     c.Eb = st.E + (size_t)tile * g.nnz * kTile + lo;
@@ -825,6 +832,7 @@ __global__ __launch_bounds__(64 * kSW, 1) void tile_sub_stream_kernel(
 
     SubCtx<Q> c;
     c.col_idx = col_idx;
+    c.col16 = g.col16;
     c.row_ptr = row_ptr;
     const size_t lo = (size_t)lane64;
     c.Eb = st.E + (size_t)tile * g.nnz * kTile + lo;
@@ -884,7 +892,7 @@ __global__ __launch_bounds__(64 * kSW, 1) void tile_sub_stream_kernel(
                 const unsigned long long below = lane ? (w & (~0ull >> (64 - lane))) : 0ull;
                 const int64_t idx = (int64_t)(base + (unsigned long long)__popcll(below));
                 have = want && idx < total;
-                if (slot_lane) gidx[f] = have ? (long long)(frame0 + idx) : -1ll;
+                if (slot_lane) gidx[f] = have ? supply_frame(st, frame0, idx) : -1ll;
                 if (want) {
                     livel[f] = have ? 1 : 0;
                     freshl[f] = have ? 1 : 0;

@@ -271,3 +271,26 @@ def test_tile8_stream_r12_equals_static(gpu_available, monkeypatch):
     d = _decoder(code, cap).mc_run(SEED, sig, frames, 9, T, nllr=True)
     for x in (b, c, d):
         np.testing.assert_array_equal(a, x)
+
+
+@pytest.mark.parametrize("code,cap,frames,T,snrs", [
+    ("wimax_2304_0.5", 256, 1500, 20, (2.5, 3.0)),    # tile_sub_stream_kernel + hand-off
+    ("wimax_2304_0.75A", 128, 700, 20, (3.0, 4.0)),   # tile8_stream_kernel + hand-off
+    ("wimax_576_0.5", 128, 2000, 30, (1.5, 2.5)),     # tile_stream_kernel
+])
+def test_supply_order_keeps_counters(gpu_available, monkeypatch, code, cap, frames, T, snrs):
+    """Longest job first (frame_order.hip: frames enter the slots in descending
+    syndrome weight of their hard decisions) changes only WHEN a frame is
+    decoded: the counters equal frame-index order (LDPC_LPT=0), the split
+    streaming loop under the same order, and the static schedule."""
+    dec = _decoder(code, cap)
+    sig = [oracle.sigma_for_snr(s) for s in snrs]
+    a = dec.mc_run(SEED, sig, frames, 21, T, nllr=True)
+    b = dec.mc_run(SEED, sig, frames, 21, T, nllr=True, split=True)
+    monkeypatch.setenv("LDPC_LPT", "0")
+    c = dec.mc_run(SEED, sig, frames, 21, T, nllr=True)
+    monkeypatch.delenv("LDPC_LPT")
+    d = dec.mc_run(SEED, sig, frames, 21, T, nllr=True, static=True)
+    for x in (b, c, d):
+        np.testing.assert_array_equal(a, x)
+    assert (a[:, 0] == frames).all()

@@ -10,6 +10,15 @@ out = {"value": round(d["value"] or 0), "n_gpus": d.get("n_gpus"), "kernel": r.g
 ph = d.get("physical")
 if ph:
     out["physical"] = (round(ph["value"]), round(ph.get("roofline", {}).get("frac", 0), 3), round(ph["avg_iters"], 2))
+if ph and ph.get("waterfall"):
+    w = ph["waterfall"]
+    out["phys_waterfall"] = (round(w["value"]), round(w.get("roofline", {}).get("frac", 0), 3), round(w["avg_iters"], 2))
+c4 = d.get("config4")
+if c4:
+    out["config4"] = (round(c4["value"]), round(c4["roofline"]["frac"], 3),
+                      [(p["snr_db"], round(p["value"]), round(p["roofline_frac"] or 0, 3)) for p in c4["points"]])
+    s4 = c4.get("static_1dB") or {}
+    out["config4_static"] = (round(s4.get("value", 0)), round((s4.get("roofline") or {}).get("frac", 0), 3))
 di = d.get("dropin")
 if di:
     out["dropin_ms"] = round(di["ms_per_call"], 2)
