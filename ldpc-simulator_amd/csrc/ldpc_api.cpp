@@ -401,7 +401,7 @@ size_t workspace_bytes(const DevGraph &g, int cap_tiles) {
     b += cap * (size_t)g.nnz * 8;                                   // E
     const size_t slots = ldpc::use_tile(g) ? std::max(scratch_slots(), cap_tiles) : scratch_slots();
     b += slots * g.max_row_deg * kTile * 8;  // T pool
-    b += 4 * (2 + (size_t)cap_tiles * g.m);                               // rare list
+    b += 4 * (2 + (size_t)cap_tiles * g.m * 4);                           // rare list
     b += 2 * cap * (size_t)g.n * 8;    // L, ch
     b += (7 * cap + cap_tiles) * 4;    // per-frame ints + tile flags
     b += cap * kw * 4;                 // ubits
@@ -631,7 +631,14 @@ int ldpc_decoder_create(const ldpc_graph *g, int32_t max_frames, ldpc_decoder **
     int rc = LDPC_OK;
     d->nslots = scratch_slots();  // E and T are allocated on first parity-mode use
     if (ldpc::use_tile(G)) d->nslots = std::max(d->nslots, d->cap_tiles);  // one scratch slot per tile workgroup
-    if (!rc) rc = dev_alloc(&d->rare, 2 + (size_t)d->cap_tiles * G.m);
+    // rare list: one entry per (tile, row), or per 16-frame sub-tile of it (cn_sub_kernel);
+    // entries pack tile * m + row into 28 bits (spa_device.h rare_code)
+    if ((int64_t)d->cap_tiles * G.m >= (int64_t)1 << 28) {
+        delete d;
+        return ldpc_fail(LDPC_ERANGE, "ldpc_decoder_create: %d frames x %d rows exceed the rare-row list", max_frames,
+                         G.m);
+    }
+    if (!rc) rc = dev_alloc(&d->rare, 2 + (size_t)d->cap_tiles * G.m * 4);
     if (!rc && hipMemset(d->rare, 0, sizeof(int) * 2) != hipSuccess)
         rc = ldpc_fail(LDPC_EDEVICE, "ldpc_decoder_create: memset failed");
     if (!rc) rc = dev_alloc(&d->L, cap * (size_t)G.n);

@@ -150,6 +150,16 @@ int edge_max_deg();
 hipError_t launch_cn_edge(const DevGraph &g, const DevState &st, int it, hipStream_t s);
 hipError_t launch_vn_edge_decode(const DevGraph &g, const DevState &st, int it, bool last, bool nllr, uint32_t *zb,
                                  int *cnt, int *gbad, hipStream_t s);
+// split CN on 16-frame sub-tiles, t in registers (cn_sub.hip): rows of the
+// 2304 codes; 0 when no shape fits the graph
+int cn_sub_shape(const DevGraph &g);
+hipError_t launch_cn_sub(const DevGraph &g, const DevState &st, int it, hipStream_t s, bool stream);
+// rare-row list entries (cn_rare_kernel): tile * m + row in bits 0..27, and
+// in bits 28..31 the 16-frame sub-tiles of the tile it covers (0 = all 64
+// frames: cn_kernel / cn_row_kernel; bit s = frames 16 s .. 16 s + 15: cn_sub_kernel)
+__host__ __device__ inline uint32_t rare_code(int tile_row, uint32_t subs) {
+    return (uint32_t)tile_row | (subs << 28);
+}
 // supply order of a streamed point (frame_order.hip): keys 2 x total uint32,
 // vals total int scratch, order total int out, temp frame_order_temp_bytes
 size_t frame_order_temp_bytes(int total);

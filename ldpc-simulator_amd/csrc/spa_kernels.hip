@@ -331,11 +331,14 @@ __global__ __launch_bounds__(256) void cn_rare_kernel(DevGraph g, DevState st, i
     const int nw = (int)gridDim.x * 4;
     double *Tt = st.T + (size_t)gw * g.max_row_deg * kTile + lane;
     for (int idx = gw; idx < count; idx += nw) {
-        const int code = st.rare_list[idx];
-        const int tile = code / g.m, row = code % g.m;
+        const uint32_t code = (uint32_t)st.rare_list[idx];
+        const int tr = (int)(code & 0x0fffffffu);
+        const uint32_t subs = code >> 28;  // 0: every frame of the tile; else the listed 16-frame sub-tiles
+        const int tile = tr / g.m, row = tr % g.m;
         const int beg = g.row_ptr[row], end = g.row_ptr[row + 1];
         const int f = tile * kTile + lane;
-        const bool live = st.done[f] == 0;
+        const bool mine = subs == 0u || ((subs >> (lane >> 4)) & 1u) != 0u;
+        const bool live = mine && st.done[f] == 0;
         const bool fresh = kStream && st.fresh[f] != 0;
         double *Et = st.E + e_base(g, tile, lane);
         const double *Lt = (kFirst ? st.ch : st.L) + (size_t)tile * g.n * kTile + lane;
@@ -890,7 +893,20 @@ void launch_cn_row(const DevGraph &g, const DevState &st, int par, hipStream_t s
                                                                                             kAtanhCoef);
 }
 
+// cn_sub_kernel (cn_sub.hip: 16-frame sub-tiles, t in registers, one tanh per
+// edge) for the long rows of the 2304 codes up to LDPC_CN_SUB tiles (read per
+// call; 0 = never; default kCnSubTiles: the streaming tail and small split
+// batches, where cn_kernel's two tanh per edge made it VALU-issue bound).
+constexpr int kCnSubTiles = 128;
+bool use_cn_sub(const DevGraph &g, int ntiles) {
+    if (use_cn_row(g) || !cn_sub_shape(g)) return false;
+    const char *e = getenv("LDPC_CN_SUB");
+    const int lim = e ? atoi(e) : kCnSubTiles;
+    return ntiles <= lim;
+}
+
 hipError_t launch_cn(const DevGraph &g, const DevState &st, int it, hipStream_t s, bool stream) {
+    if (use_cn_sub(g, st.ntiles)) return launch_cn_sub(g, st, it, s, stream);
     if (use_cn_row(g) || use_cn_row16(g, st.ntiles)) {
         const int par = it & 1;
         if (stream)

@@ -201,5 +201,41 @@ def test_cn_row16_bit_identical_to_sub_tile(gpu_available, monkeypatch, snr, T, 
     dec = _decoder(code, B)
     a = dec.decode(llr, T, nllr=True, post=True, hist=True, msgs=True)
     monkeypatch.setenv("LDPC_CN_ROW16", "1")
+    monkeypatch.setenv("LDPC_CN_SUB", "0")  # cn_sub_kernel would take these small batches
     b = dec.decode(llr, T, nllr=True, post=True, hist=True, msgs=True, split=True)
     _assert_identical(a, b)
+
+
+@pytest.mark.parametrize("code,snr,T,B", [("wimax_2304_0.5", 0.0, 4, 70), ("wimax_2304_0.5", 3.0, 25, 40),
+                                          ("wimax_2304_0.5", 1.0, 1, 64),
+                                          ("wimax_2304_0.75A", 2.0, 6, 72), ("wimax_2304_0.75B", 3.5, 10, 64)])
+def test_cn_sub_bit_identical_to_cn_kernel(gpu_available, monkeypatch, code, snr, T, B):
+    """cn_sub_kernel (16-frame sub-tiles, t in registers, one tanh per edge:
+    the split CN of the long-row codes up to LDPC_CN_SUB tiles) == cn_kernel
+    (one wavefront per row, two tanh per edge), every output, with rare rows
+    (exact zeros, tiny LLRs: the sub-tile's frames go to cn_rare_kernel) and
+    ragged batches."""
+    H = hstd_for(code)
+    llr = _random_llr(H, B, snr, seed=int(100 * snr) + 5000 + T)
+    llr[1, ::5] = 0.0
+    llr[3, :] = 1e-13
+    llr[B - 1, ::9] = 0.0  # a rare row in the last (possibly partial) sub-tile
+    dec = _decoder(code, B)
+    monkeypatch.setenv("LDPC_SMALL_COLS", "0")  # the split path with the per-tile vn_kernel
+    a = dec.decode(llr, T, nllr=True, post=True, hist=True, msgs=True, split=True)
+    monkeypatch.setenv("LDPC_CN_SUB", "0")
+    b = dec.decode(llr, T, nllr=True, post=True, hist=True, msgs=True, split=True)
+    _assert_identical(a, b)
+
+
+def test_cn_sub_stream_counters(gpu_available, monkeypatch):
+    """The streaming split loop (fresh frames, refills, compaction, the
+    column-parallel tail VN) with cn_sub_kernel == with cn_kernel."""
+    import oracle as _o
+    code = "wimax_2304_0.5"
+    dec = _decoder(code, 256)
+    sig = [_o.sigma_for_snr(s) for s in (2.5, 3.0)]
+    a = dec.mc_run(20260213, sig, 900, 33, 20, nllr=True, split=True)
+    monkeypatch.setenv("LDPC_CN_SUB", "0")
+    b = dec.mc_run(20260213, sig, 900, 33, 20, nllr=True, split=True)
+    np.testing.assert_array_equal(a, b)
