@@ -264,15 +264,18 @@ def committed_traffic(nnz, frames, kernel="cn"):
     pdir = os.path.join(ROOT, "profiles")
     best = None
     for d in sorted(os.listdir(pdir), key=profile_order) if os.path.isdir(pdir) else []:
-        f = os.path.join(pdir, d, "traffic.json")
-        if not os.path.exists(f):
+        if not os.path.isdir(os.path.join(pdir, d)):
             continue
-        t = json.load(open(f))
-        if t.get("edges") == nnz and t.get("frames") == frames:
-            k = t["kernels"]
-            cn = k.get(kernel) or (k.get("cn_kernel<false>") if kernel == "cn" else None)
-            if cn:
-                best = (cn["traffic_bytes"], os.path.relpath(f, ROOT))
+        for fn in sorted(os.listdir(os.path.join(pdir, d))):
+            if not (fn.startswith("traffic") and fn.endswith(".json")):
+                continue
+            f = os.path.join(pdir, d, fn)
+            t = json.load(open(f))
+            if t.get("edges") == nnz and t.get("frames") == frames:
+                k = t.get("kernels", {})
+                cn = k.get(kernel) or (k.get("cn_kernel<false>") if kernel == "cn" else None)
+                if cn:
+                    best = (cn["traffic_bytes"], os.path.relpath(f, ROOT))
     return best or (None, None)
 
 

@@ -93,6 +93,12 @@ __device__ __forceinline__ int t8_wave(int hw) { return (hw & 3) * 4 + (hw >> 2)
 // the prefetched E_old).  NT = non-temporal (the message stream).
 typedef unsigned int t8u2 __attribute__((ext_vector_type(2)));
 constexpr int kNT = 2;
+// LDPC_EST_SC1 (A/B): E_new stores sc1 (aux bit 4: written through and dropped
+// from L2) instead of nt, which keeps the line (MI355X_MICROARCH.md)
+#ifndef LDPC_EST_SC1
+#define LDPC_EST_SC1 0
+#endif
+constexpr int kEStAux = LDPC_EST_SC1 ? 16 : kNT;
 // a voffset past every buffer's num_records: the hardware drops such a store
 // (and a load returns 0) -- masked stores without a branch
 constexpr uint32_t kOOB = 0xfffffff0u;
@@ -469,10 +475,10 @@ __device__ __forceinline__ void t8_p3(T8Ctx<K> &c, int r, double (&t)[K]) {
     if (rc.cnt > 0) {  // slots past the piece (and frames that stopped) store out of range: dropped
         const uint32_t eoff = t8_eoff(c, rc);
 #pragma unroll
-        for (int i = 0; i < K; ++i) t8_st<kNT>(c.rE, (i < nj && c.live) ? t8_es(c, eoff, i) : kOOB, t[i]);
+        for (int i = 0; i < K; ++i) t8_st<kEStAux>(c.rE, (i < nj && c.live) ? t8_es(c, eoff, i) : kOOB, t[i]);
     }
     if (c.live) {
-        if (idw && c.j == 0) t8_st<kNT>(c.rE, ((uint32_t)(rc.beg + rc.deg - 1) << 6) + c.eo8, EI);
+        if (idw && c.j == 0) t8_st<kEStAux>(c.rE, ((uint32_t)(rc.beg + rc.deg - 1) << 6) + c.eo8, EI);
     }
     // S order: row r-1's P3 by the overlapping wavefronts
     T8_STAMP(q2);

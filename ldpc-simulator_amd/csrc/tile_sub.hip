@@ -106,7 +106,18 @@ static_assert(((kStaticBF & kStreamBF) & 1) != 0, "the branch-free hop needs the
 // same, spin waits at a lower issue priority +0.2 %).
 __device__ __forceinline__ int sub_wave(int hw) { return (hw & 3) * 4 + (hw >> 2); }
 __device__ __forceinline__ double ld_sub_msg(const double *p) { return __builtin_nontemporal_load(p); }
-__device__ __forceinline__ void st_sub_msg(double *p, double v) { __builtin_nontemporal_store(v, p); }
+// LDPC_EST_SC1 (A/B): E_new stored sc1 (the line is written through and
+// dropped from the XCD's L2, MI355X_MICROARCH.md: nt and plain stores keep it,
+// evicting the posteriors the L gather re-reads)
+#ifndef LDPC_EST_SC1
+#define LDPC_EST_SC1 0
+#endif
+__device__ __forceinline__ void st_sub_msg(double *p, double v) {
+    if (LDPC_EST_SC1)
+        __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else
+        __builtin_nontemporal_store(v, p);
+}
 
 // Column indices of the rows in flight, staged per wavefront in LDS as 16-bit
 // values one row ahead of their P1 (a ring of 3 rows: P3(r-1), P1(r+1) and the
