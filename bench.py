@@ -103,6 +103,14 @@ def parse():
                     help="frames per GPU per config-4 point (one GPU's shard of 262,144 over 8 GPUs)")
     ap.add_argument("--config4-slots", type=int, default=2048,
                     help="streaming slots of the config-4 decoder (256 CUs x one 8-frame tile8 workgroup)")
+    ap.add_argument("--config2", type=int, default=1,
+                    help="parity mode: BASELINE config 2 (wimax_576_0.5, T=50, 65,536 frames, 0 dB) timed for "
+                         "--config2-steps steps under 'config2' (0 = none)")
+    ap.add_argument("--config2-steps", type=int, default=3)
+    ap.add_argument("--config5", type=int, default=1,
+                    help="parity mode: BASELINE config 5 (DVB-S2 n=64800 r1/2 profile, physical mode only: its "
+                         "H_std would have ~5e8 edges) under 'config5' (0 = none)")
+    ap.add_argument("--config5-frames", type=int, default=8192, help="config-5 frames per GPU per step")
     ap.add_argument("--dropin-calls", type=int, default=20,
                     help="parity mode: one-frame decode() calls timed under 'dropin' (main.py's call pattern; 0 = none)")
     ap.add_argument("--stub", action="store_true",
@@ -510,7 +518,7 @@ def config4_extra(args, local, world, rank, dist):
         out["roofline"]["traffic_source"] = tsrc
     # the fused static decoder (tile8_kernel) at 1 dB: one 32,768-frame launch, all 50 iterations
     sdec = Decoder(g, F)
-    sdec.mc_run(SEED, [sig(1.0)], F, base - 2 * F - 4096, args.iters, static=True)  # warm-up
+    sdec.mc_run(SEED, [sig(1.0)], 2048, base - 2 * F - 4096, args.iters, static=True)  # warm-up (tile8 from 17 tiles)
     barrier(dist, local)
     sdec.profile_read()
     sdec.profile(True)
@@ -534,6 +542,113 @@ def config4_extra(args, local, world, rank, dist):
         tr, tsrc = committed_traffic(nnz, F, "tile")
         st["roofline"]["traffic"], st["roofline"]["traffic_source"] = tr, tsrc
     out["static_1dB"] = st
+    return out
+
+
+def config2_extra(args, local, world, rank, dist):
+    """BASELINE config 2: wimax_576_0.5, SPA fp64, T=50 with early termination,
+    65,536 frames per GPU per step at the reference axis' 0 dB (FER 1.0 in the
+    reference: every frame runs 50 iterations), static schedule -> one
+    tile_kernel launch per step (64 frames per workgroup, CN + VN fused)."""
+    import ldpc_amd
+    from ldpc_amd import _lib
+    from ldpc_amd.device import Decoder, Graph
+    edd = ldpc_amd.load_committed_code("wimax_576_0.5")
+    H = edd._h_std
+    n, k, nnz = edd._n, edd._k, H.nnz
+    g = Graph(H, device=local)
+    F = 65536
+    dec = Decoder(g, F)
+    sig = 1.0 / math.sqrt(2.0)  # 0 dB, speed 1 (channel.py:113)
+    base = 1 << 44
+    dec.mc_run(SEED, [sig], F, base - F, args.iters, static=True)  # warm-up
+    barrier(dist, local)
+    dec.profile_read()
+    dec.profile(True)
+    t1 = time.perf_counter()
+    loc = np.zeros((1, 7), np.int64)
+    tot = np.zeros((1, 7), np.int64)
+    for st in range(args.config2_steps):
+        c = dec.mc_run(SEED, [sig], F, base + (st * world + rank) * F, args.iters, static=True)
+        loc += c
+        tot += allreduce_counters(dist, c, local)
+    barrier(dist, local)
+    dt = max_over_ranks(dist, time.perf_counter() - t1, local)
+    dec.profile(False)
+    tms, tl = dec.profile_read()["tile"]
+    dec.close()
+    f = int(tot[0, 0])
+    byts = F * args.config2_steps * (8 * n + math.ceil(n / 8) + 8) + 16.0 * nnz * int(loc[0, 6])
+    out = {"what": "BASELINE config 2: wimax_576_0.5 SPA fp64, T=50 + early termination, 0 dB (FER 1.0 in the "
+                   "reference), 65,536 frames per GPU per step, static schedule",
+           "code": "wimax_576_0.5", "n": n, "k": k, "edges_H_std": nnz, "snr_db": 0.0, "max_iter": args.iters,
+           "frames_per_gpu_step": F, "steps": args.config2_steps, "n_gpus": world,
+           "value": f / dt, "unit": "codewords/s", "info_bits_per_s": f * k / dt,
+           "ms_per_step": dt / args.config2_steps * 1e3, "avg_iters": int(tot[0, 6]) / max(f, 1),
+           "fer": int(tot[0, 1]) / max(f, 1),
+           "kernel": _lib.lib().ldpc_tile_kernel_name(g.handle).decode(), "launches": tl}
+    if tl:
+        tr, tsrc = committed_traffic(nnz, F, "tile")
+        out["roofline"] = {"bound": "hbm", "achieved": byts / (tms / 1e3) / 1e9, "peak": HBM_PEAK_GBS,
+                           "unit": "GB/s", "frac": byts / (tms / 1e3) / 1e9 / HBM_PEAK_GBS,
+                           "avg_launch_ms": tms / tl, "bytes_per_launch": byts / tl,
+                           "traffic": tr, "traffic_source": tsrc,
+                           "bytes_model": "per frame 8 n + 16 B x H_std edges x iterations + ceil(n/8) + 8 "
+                                          "(SURVEY 8d), CN and VN fused"}
+    return out
+
+
+def config5_extra(args, local, world, rank, dist):
+    """BASELINE config 5: DVB-S2 n=64800 rate-1/2 at 50 max iterations, 8,192
+    frames -- in physical mode only (its H_std = [A | I] would
+    have ~5e8 edges).  The code has DVB-S2's exact rate-1/2 normal-frame
+    structure and degree profile with a SEEDED address table (the ETSI table
+    is not available offline: ldpc_amd/ira.py), so this is a stress test of
+    the long irregular code's decoder, with no parity to the reference.  State
+    in HBM (phys_cn_tile / phys_vn_tile), on-device IRA encoder."""
+    from ldpc_amd import ira
+    from ldpc_amd.device import Decoder, Graph
+    H = ira.dvbs2_profile_matrix()
+    m, n = H.shape
+    k = n - m
+    g = Graph(H, device=local)
+    F = args.config5_frames
+    dec = Decoder(g, F)
+    sig = 1.0 / math.sqrt(2.0 * (10.0 ** (args.snr * 0.1)))
+    base = 1 << 45
+    dec.phys_mc_run(g, SEED, [sig], F, base - F, args.iters)  # warm-up
+    barrier(dist, local)
+    dec.profile_read()
+    dec.profile(True)
+    t1 = time.perf_counter()
+    loc = np.zeros((1, 7), np.int64)
+    tot = np.zeros((1, 7), np.int64)
+    steps = 2
+    for st in range(steps):
+        c = dec.phys_mc_run(g, SEED, [sig], F, base + (st * world + rank) * F, args.iters)
+        loc += c
+        tot += allreduce_counters(dist, c, local)
+    barrier(dist, local)
+    dt = max_over_ranks(dist, time.perf_counter() - t1, local)
+    dec.profile(False)
+    prof = dec.profile_read()
+    dec.close()
+    cms, cl = prof["phys_cn"]
+    f = int(tot[0, 0])
+    out = {"what": "BASELINE config 5: DVB-S2 n=64800 r1/2 profile (seeded address table), physical mode "
+                   "(fp32, sparse graph, state in HBM) -- no reference parity",
+           "code": "dvbs2_profile_64800_0.5", "n": n, "k": k, "edges_H": int(H.nnz), "snr_db": args.snr,
+           "max_iter": args.iters, "frames_per_gpu_step": F, "steps": steps, "n_gpus": world,
+           "value": f / dt, "unit": "codewords/s", "info_bits_per_s": f * k / dt,
+           "ms_per_step": dt / steps * 1e3, "avg_iters": int(tot[0, 6]) / max(f, 1),
+           "fer": int(tot[0, 1]) / max(f, 1), "dtype": "f32"}
+    if cl:
+        cn_bytes = 12.0 * H.nnz * int(loc[0, 6])
+        out["roofline"] = {"bound": "hbm", "kernel": "phys_cn_tile_kernel", "launches": cl,
+                           "achieved": cn_bytes / (cms / 1e3) / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                           "frac": cn_bytes / (cms / 1e3) / 1e9 / HBM_PEAK_GBS,
+                           "bytes_model": "12 B x H edges x frame-iterations (L[col] gather + E_old read + "
+                                          "E_new write, fp32), over the CN launches' HIP-event time"}
     return out
 
 
@@ -720,6 +835,10 @@ def main():
     if args.config4_snr.strip() and pgraph is None and not ira_code:
         dec.close()  # idempotent (the physical key may have closed it)
         config4 = config4_extra(args, local, world, rank, dist)
+    config2 = config2_extra(args, local, world, rank, dist) if args.config2 and pgraph is None and not ira_code \
+        else None
+    config5 = config5_extra(args, local, world, rank, dist) if args.config5 and pgraph is None and not ira_code \
+        else None
     dropin = dropin_extra(args, graph, n) if args.dropin_calls > 0 and pgraph is None else None
 
     frames_total = int(totals[0, 0])
@@ -794,8 +913,12 @@ def main():
         out["snr_points"] = snr_points
     if physical is not None:
         out["physical"] = physical
+    if config2 is not None:
+        out["config2"] = config2
     if config4 is not None:
         out["config4"] = config4
+    if config5 is not None:
+        out["config5"] = config5
     if dropin is not None:
         out["dropin"] = dropin
     if not tile_launches and pgraph is None and cn_launches:

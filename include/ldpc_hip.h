@@ -170,6 +170,14 @@ int ldpc_generate_frames(ldpc_decoder *d, uint64_t seed, int32_t snr_point, doub
  * completion instead.  Both decode the same frames: counters are identical.
  */
 #define LDPC_MC_NCOUNT 7
+/* The streaming schedule's supply order of one point (ABI 4): the point's
+ * local frame indices 0..count-1 (global frame0 + i) sorted by descending
+ * syndrome weight of the channel hard decisions (llr > 0) on H_std, ties in
+ * index order -- longest job first; order_out [count] int32, host memory.
+ * ldpc_mc_run streams frames in this order unless LDPC_LPT=0 (the counters
+ * are order-independent sums). */
+int ldpc_frame_order(ldpc_decoder *d, uint64_t seed, int32_t snr_point, double sigma, int64_t frame0,
+                     int32_t count, int32_t *order_out, void *stream);
 int ldpc_mc_run(ldpc_decoder *d, uint64_t seed, int32_t n_points, const double *sigmas,
                 int64_t frames_per_point, int64_t frame0, int32_t max_iter, uint32_t flags,
                 int64_t *counters_out, void *stream);

@@ -1060,6 +1060,24 @@ int mc_stream_point(ldpc_decoder *d, uint64_t seed, int p, double sigma, int64_t
 
 }  // namespace
 
+int ldpc_frame_order(ldpc_decoder *d, uint64_t seed, int32_t snr_point, double sigma, int64_t frame0,
+                     int32_t count, int32_t *order_out, void *stream) {
+    if (!d || count < 0 || snr_point < 0 || frame0 < 0 || !(sigma > 0.0) || (count > 0 && !order_out))
+        return ldpc_fail(LDPC_EINVAL, "ldpc_frame_order: bad arguments");
+    const DevGraph &G = d->g->dg;
+    if (!G.std_form || !G.a_packed || G.m > 65535)
+        return ldpc_fail(LDPC_EINVAL, "ldpc_frame_order: graph is not [A | I_m] with m <= 65535");
+    if (count == 0) return LDPC_OK;
+    DeviceGuard dg(d->g->device);
+    hipStream_t s = (hipStream_t)stream;
+    if (int rc = ensure_order(d, count)) return rc;
+    HIP_TRY(ldpc::launch_frame_order(G, seed, snr_point, sigma, frame0, count, d->ord_keys, d->ord_vals, d->ord,
+                                     d->ord_tmp, d->ord_tmp_bytes, s));
+    HIP_TRY(hipMemcpyAsync(order_out, d->ord, sizeof(int32_t) * (size_t)count, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    return LDPC_OK;
+}
+
 int ldpc_mc_run(ldpc_decoder *d, uint64_t seed, int32_t n_points, const double *sigmas, int64_t frames_per_point,
                 int64_t frame0, int32_t max_iter, uint32_t flags, int64_t *counters_out, void *stream) {
     if (!d || n_points <= 0 || !sigmas || frames_per_point < 0 || frame0 < 0 || max_iter < 1 || !counters_out)

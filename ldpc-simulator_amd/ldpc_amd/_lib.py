@@ -38,7 +38,7 @@ EXPORTED = (
     "ldpc_graph_create", "ldpc_graph_destroy", "ldpc_graph_info", "ldpc_cn_kernel_name",
     "ldpc_phys_kernel_name", "ldpc_tile_lds_bytes", "ldpc_tile_kernel_name",
     "ldpc_decoder_bytes", "ldpc_decoder_create", "ldpc_decoder_destroy", "ldpc_decoder_capacity",
-    "ldpc_decode_f64", "ldpc_generate_frames", "ldpc_mc_run",
+    "ldpc_decode_f64", "ldpc_generate_frames", "ldpc_mc_run", "ldpc_frame_order",
     "ldpc_profile_enable", "ldpc_profile_read",
     "ldpc_phys_lds_bytes", "ldpc_phys_decode", "ldpc_phys_mc_run",
     "ldpc_comm_unique_id", "ldpc_comm_init", "ldpc_comm_allreduce", "ldpc_comm_barrier", "ldpc_comm_destroy",
@@ -90,6 +90,7 @@ def _declare(lib):
                                                 c_vp, c_vp, c_vp]),
         "ldpc_mc_run": (ctypes.c_int, [c_vp, c_u64, c_i32, P(c_dbl), c_i64, c_i64, c_i32, c_u32,
                                        P(c_i64), c_vp]),
+        "ldpc_frame_order": (ctypes.c_int, [c_vp, c_u64, c_i32, c_dbl, c_i64, c_i32, c_vp, c_vp]),
         "ldpc_profile_enable": (ctypes.c_int, [c_vp, ctypes.c_int]),
         "ldpc_phys_lds_bytes": (c_i64, [c_vp]),
         "ldpc_phys_decode": (ctypes.c_int, [c_vp, c_i32, c_vp, c_i32, c_u32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),

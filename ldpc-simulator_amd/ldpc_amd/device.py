@@ -233,6 +233,15 @@ class Decoder:
             out.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)), None))
         return out
 
+    def frame_order(self, seed, snr_point, sigma, frame0, count):
+        """The streaming schedule's supply order of a point (ldpc_frame_order):
+        local frame indices by descending syndrome weight of their channel hard
+        decisions, ties in index order."""
+        out = np.empty(int(count), np.int32)
+        check("ldpc_frame_order", _lib.gpu().ldpc_frame_order(
+            self._h, int(seed), int(snr_point), float(sigma), int(frame0), int(count), _lib.ptr(out), None))
+        return out
+
     def phys_mc_run(self, phys_graph, seed, sigmas, frames_per_point, frame0, max_iter, hbm=False):
         """Physical mode (§8 f4): same on-device frames, decoded on the sparse graph.
 

@@ -294,3 +294,21 @@ def test_supply_order_keeps_counters(gpu_available, monkeypatch, code, cap, fram
     for x in (b, c, d):
         np.testing.assert_array_equal(a, x)
     assert (a[:, 0] == frames).all()
+
+
+@pytest.mark.parametrize("code,snr,count", [("wimax_2304_0.5", 3.0, 700), ("wimax_2304_0.75A", 2.5, 300),
+                                            ("wimax_576_0.5", 1.0, 1000)])
+def test_frame_order_matches_host_ranking(gpu_available, code, snr, count):
+    """frame_order.hip's supply order == the stable descending ranking by the
+    syndrome weight of H_std (llr > 0), recomputed on the host from the
+    oracle's restatement of the device frame source (oracle/channel_oracle.c)."""
+    H = hstd_for(code)
+    sig = oracle.sigma_for_snr(snr)
+    frame0 = 123457
+    order = _decoder(code, 64).frame_order(SEED, 2, sig, frame0, count)
+    _, _, llr = oracle.generate_frames(H, SEED, 2, sig, frame0, count)
+    hard = (llr > 0.0).astype(np.int64)
+    w = ((H @ hard.T) % 2).sum(axis=0)
+    want = np.argsort(-w, kind="stable")
+    np.testing.assert_array_equal(order, want)
+    assert w[order[0]] >= w[order[-1]]

@@ -19,6 +19,10 @@ if c4:
                       [(p["snr_db"], round(p["value"]), round(p["roofline_frac"] or 0, 3)) for p in c4["points"]])
     s4 = c4.get("static_1dB") or {}
     out["config4_static"] = (round(s4.get("value", 0)), round((s4.get("roofline") or {}).get("frac", 0), 3))
+for key in ("config2", "config5"):
+    c = d.get(key)
+    if c:
+        out[key] = (round(c["value"]), round((c.get("roofline") or {}).get("frac", 0), 3), round(c["avg_iters"], 2))
 di = d.get("dropin")
 if di:
     out["dropin_ms"] = round(di["ms_per_call"], 2)
