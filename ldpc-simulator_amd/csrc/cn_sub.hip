@@ -190,8 +190,13 @@ __global__ __launch_bounds__(64 * W, WPS) void cn_sub_kernel(DevGraph g, DevStat
 
 // The shapes: rows <= 8*4*20 = 640 edges (wimax_2304_0.5: 416-632) in 8
 // wavefronts x 20 slots; rows <= 8*4*30 = 960 (the r3/4 codes: <= 931) in 8 x 30.
+// LDPC_CS_W16 (A/B): the r3/4 rows in 16 wavefronts x 15 slots instead.
+#ifndef LDPC_CS_W16
+#define LDPC_CS_W16 0
+#endif
 int cn_sub_shape(const DevGraph &g) {
     if (g.max_row_deg <= 8 * kCsQ * 20) return 20;
+    if (LDPC_CS_W16 && g.max_row_deg <= 16 * kCsQ * 15) return 15;
     if (g.max_row_deg <= 8 * kCsQ * 30) return 30;
     return 0;
 }
@@ -207,6 +212,11 @@ static hipError_t launch_cn_sub_t(const DevGraph &g, const DevState &st, int par
         case 30:
             cn_sub_kernel<kFirst, kStream, 8, 30, 6, 4><<<grid, 64 * 8, 0, s>>>(g, st, par, ci, rp, kAtanhCoef);
             break;
+#if LDPC_CS_W16
+        case 15:
+            cn_sub_kernel<kFirst, kStream, 16, 15, 3, 4><<<grid, 64 * 16, 0, s>>>(g, st, par, ci, rp, kAtanhCoef);
+            break;
+#endif
         default:
             return hipErrorInvalidValue;
     }

@@ -248,15 +248,20 @@ struct T8Pre {
     double eo[K];
     double lid, eid;  // wavefront 0: the identity column's posterior and E_old
 };
-template <int K>
+// Slots [I0, I1) of the E_old loads (the L-gathering variant may issue its
+// first LDPC_T8_PF slots one body early, the rest at P1: a register budget A/B).
+#ifndef LDPC_T8_PF
+#define LDPC_T8_PF 0
+#endif
+template <int K, int I0 = 0, int I1 = K, bool kId = true>
 __device__ __forceinline__ void t8_prefetch(const T8Ctx<K> &c, int r, T8Pre<K> &p) {
     const T8Chunk rc = t8_chunk(c.row_ptr, r, c.wave);
     if (rc.cnt > 0) {  // iteration 0 forms M = L - 0.0 (== L exactly) and reads no E_old
         const uint32_t eoff = t8_eoff(c, rc);
 #pragma unroll
-        for (int i = 0; i < K; ++i) p.eo[i] = c.first ? 0.0 : t8_ld<kNT>(c.rE, t8_es(c, eoff, i));
+        for (int i = I0; i < I1; ++i) p.eo[i] = c.first ? 0.0 : t8_ld<kNT>(c.rE, t8_es(c, eoff, i));
     }
-    if (c.wave == c.idwave && rc.deg > 0) {  // identity edge (a fresh streaming frame has L = ch: gen_slots)
+    if (kId && c.wave == c.idwave && rc.deg > 0) {  // identity edge (a fresh streaming frame has L = ch: gen_slots)
         p.lid = t8_ld(c.first ? c.rC : c.rL, ((uint32_t)(c.k + r) << 9) + c.lo8);
         p.eid = c.first ? 0.0 : t8_ld<kNT>(c.rE, ((uint32_t)(rc.beg + rc.deg - 1) << 6) + c.eo8);
     }
@@ -265,36 +270,58 @@ __device__ __forceinline__ void t8_prefetch(const T8Ctx<K> &c, int r, T8Pre<K> &
 // P1: t = tanh((L[col] - E_old)/2) for this lane's slots, columns into col[];
 // returns whether some lane's own edge has |t| <= 1e-10 (:159).  Every slot is
 // evaluated (branch-free): slots past the piece hold valid data and end as 1.0.
+// LDPC_T8_KDISP (A/B): P1 and the hop run only the slots the row's pieces can
+// use -- KK = K - 1 when the row's piece length CS < K (wave-uniform; 561 of the
+// 576 rows of wimax_2304_0.75A have CS = 7 of K = 8), K otherwise -- instead of
+// all K (the padded slots cost a tanh and a chain multiply each).
+#ifndef LDPC_T8_KDISP
+#define LDPC_T8_KDISP 0
+#endif
+template <int K, int KK, bool LA>
+__device__ __forceinline__ void t8_p1_slots(const T8Ctx<K> &c, int r, const T8Chunk &rc, const T8Pre<K> &pre,
+                                            double (&t)[K], bool &tiny, bool skip_last = false) {
+    const int nj = t8_nj(c, rc);
+    const int njt = c.live ? nj : 0;  // the |t| <= 1e-10 vote: frame-less lanes abstain
+    const uint16_t *lc = t8_lcols(c, r, rc);
+    double Lv[KK];
+    int col[KK];
+#pragma unroll
+    for (int i = 0; i < KK; ++i) col[i] = lc[i];
+    if constexpr (LA) {
+#pragma unroll
+        for (int i = 0; i < KK; ++i) Lv[i] = c.LA[(size_t)col[i] * kF8];
+    } else {
+        const __amdgpu_buffer_rsrc_t rs = c.first ? c.rC : c.rL;  // iteration 0: M = ch (:85-90)
+#pragma unroll
+        for (int i = 0; i < KK; ++i) Lv[i] = t8_ld(rs, ((uint32_t)col[i] << 9) + c.lo8);
+    }
+#pragma unroll
+    for (int i = 0; i < KK; ++i) {
+        if (i == KK - 1 && skip_last) {  // wave-uniform: no piece reaches slot K-1 in this row
+            t[i] = 1.0;
+            continue;
+        }
+        // :85-90 / :260-268 (eo = 0.0 on iteration 0; a fresh streaming frame M = L)
+        const double M = c.fresh ? Lv[i] : Lv[i] - pre.eo[i];
+        const double tv = tanh_half_clipped(M, c.ttab);  // :138-146 (spa_math.h)
+        tiny |= i < njt && !(fabs(tv) > kTiny);
+        t[i] = i < nj ? tv : 1.0;  // past the piece: an exact no-op in the product
+        t8_slot_fence();
+    }
+#pragma unroll
+    for (int i = KK; i < K; ++i) t[i] = 1.0;
+}
+
 template <int K, bool LA>
 __device__ __forceinline__ bool t8_p1(const T8Ctx<K> &c, int r, const T8Pre<K> &pre, double (&t)[K]) {
     bool tiny = false;
     const int sv = t8_stage_issue(c, r + 1);
     const T8Chunk rc = t8_chunk(c.row_ptr, r, c.wave);
     if (rc.cnt > 0) {
-        const int nj = t8_nj(c, rc);
-        const int njt = c.live ? nj : 0;  // the |t| <= 1e-10 vote: frame-less lanes abstain
-        const uint16_t *lc = t8_lcols(c, r, rc);
-        double Lv[K];
-        int col[K];
-#pragma unroll
-        for (int i = 0; i < K; ++i) col[i] = lc[i];
-        if constexpr (LA) {
-#pragma unroll
-            for (int i = 0; i < K; ++i) Lv[i] = c.LA[(size_t)col[i] * kF8];
-        } else {
-            const __amdgpu_buffer_rsrc_t rs = c.first ? c.rC : c.rL;  // iteration 0: M = ch (:85-90)
-#pragma unroll
-            for (int i = 0; i < K; ++i) Lv[i] = t8_ld(rs, ((uint32_t)col[i] << 9) + c.lo8);
-        }
-#pragma unroll
-        for (int i = 0; i < K; ++i) {
-            // :85-90 / :260-268 (eo = 0.0 on iteration 0; a fresh streaming frame M = L)
-            const double M = c.fresh ? Lv[i] : Lv[i] - pre.eo[i];
-            const double tv = tanh_half_clipped(M, c.ttab);  // :138-146 (spa_math.h)
-            tiny |= i < njt && !(fabs(tv) > kTiny);
-            t[i] = i < nj ? tv : 1.0;  // past the piece: an exact no-op in the product
-            t8_slot_fence();
-        }
+        if (LDPC_T8_KDISP == 1 && K > 1 && rc.CS < K)
+            t8_p1_slots<K, (K > 1 ? K - 1 : K), LA>(c, r, rc, pre, t, tiny);
+        else
+            t8_p1_slots<K, K, LA>(c, r, rc, pre, t, tiny, LDPC_T8_KDISP == 2 && rc.CS < K);
     } else {
 #pragma unroll
         for (int i = 0; i < K; ++i) t[i] = 1.0;
@@ -353,11 +380,20 @@ __device__ __forceinline__ void t8_hop(T8Ctx<K> &c, int r, const double (&t)[K],
         // branch-free: every lane group multiplies all K slots (slots past its
         // piece, and every slot of a group past the chunk, hold 1.0: exact
         // no-ops), so the product ends in group 7 whatever the chunk's length
+        if (LDPC_T8_KDISP != 0 && K > 1 && rc.CS < K) {  // slot K-1 holds 1.0 in every group: skip it
 #pragma unroll
-        for (int jj = 0; jj < kQ8; ++jj) {
+            for (int jj = 0; jj < kQ8; ++jj) {
 #pragma unroll
-            for (int i = 0; i < K; ++i) P = P * t[i];
-            if (jj + 1 < kQ8) P = t8_group_up(P, jj);
+                for (int i = 0; i < K - 1; ++i) P = P * t[i];
+                if (jj + 1 < kQ8) P = t8_group_up(P, jj);
+            }
+        } else {
+#pragma unroll
+            for (int jj = 0; jj < kQ8; ++jj) {
+#pragma unroll
+                for (int i = 0; i < K; ++i) P = P * t[i];
+                if (jj + 1 < kQ8) P = t8_group_up(P, jj);
+            }
         }
     }
     if ((threadIdx.x & 63) == 0) {
@@ -524,12 +560,13 @@ __device__ __forceinline__ void t8_body(T8Ctx<K> &c, int r, double (&t)[D][K], b
     T8Pre<K> pre;
     T8_STAMP(a0);
     if (LA && r + 1 < c.m) t8_prefetch(c, r + 1, pre);
+    if (!LA && LDPC_T8_PF > 0 && r + 1 < c.m) t8_prefetch<K, 0, (LDPC_T8_PF < K ? LDPC_T8_PF : K), false>(c, r + 1, pre);
     T8_STAMP(a1);
     T8_ADD(c, 7, a0, a1);
     if (r < c.m) t8_hop(c, r, t[B], y[B]);
     if (r >= D - 1) t8_p3(c, r - (D - 1), t[N]);
     T8_STAMP(a2);
-    if (!LA && r + 1 < c.m) t8_prefetch(c, r + 1, pre);
+    if (!LA && r + 1 < c.m) t8_prefetch<K, (LDPC_T8_PF < K ? LDPC_T8_PF : K), K, true>(c, r + 1, pre);
     if (r + 1 < c.m) y[N] = t8_p1<K, LA>(c, r + 1, pre, t[N]);
     T8_STAMP(a3);
     T8_ADD(c, 6, a2, a3);

@@ -715,7 +715,10 @@ bool use_tile_stream(const DevGraph &g) {
     // + the kernel's static per-lane state (itl, freshl: 2 x 64 ints; gidx: 64
     // frame indices; the refill flag)
     if (lds) return lds + 2 * kTile * sizeof(int) + kTile * sizeof(long long) + 16 <= kTileLdsMax;
-    if (g.ef == 8) return tile8_stream_lds_bytes(g) > 0;  // tile8.hip: tile8_stream_kernel
+    if (g.ef == 8) {  // tile8.hip: tile8_stream_kernel (LDPC_TILE8_STREAM=0: the split streaming loop)
+        const char *e8 = getenv("LDPC_TILE8_STREAM");
+        return !(e8 && atoi(e8) == 0) && tile8_stream_lds_bytes(g) > 0;
+    }
     return sub16(g);
 }
 

@@ -96,6 +96,12 @@ constexpr int kStaticBF = SUB_STATIC_BF;
 #define SUB_STREAM_BF 3
 #endif
 constexpr int kStreamBF = SUB_STREAM_BF;
+// LDPC_SUB_KDISP (A/B): rows whose pieces are shorter than K (590 of 1152 rows
+// of wimax_2304_0.5 have CS = 9 of K = 10) skip the last slot's tanh and its
+// chain multiplies (one wave-uniform branch per row) instead of padding it.
+#ifndef LDPC_SUB_KDISP
+#define LDPC_SUB_KDISP 0
+#endif
 // the branch-free hop (Q = 4) multiplies all K slots: P1 must pad them (bit 0)
 static_assert(((kStaticBF & kStreamBF) & 1) != 0, "the branch-free hop needs the branch-free P1");
 // Logical wavefront (chunk position in a row) of hardware wavefront hw: the
@@ -310,6 +316,10 @@ __device__ __forceinline__ bool sub_p1(const SubCtx<Q> &c, int r, const SubChunk
         // the chunk (slots past CS hold clamped, valid data and end as 1.0)
 #pragma unroll
         for (int g0 = 0; g0 < K; g0 += kSG) {
+            if (LDPC_SUB_KDISP && kSG == 1 && g0 == K - 1 && rc.CS < K) {  // no piece reaches slot K-1
+                t[g0] = 1.0;
+                continue;
+            }
             if ((BF & 1) || g0 < rc.CS) {
                 constexpr int G0 = kSG;
                 double d[G0];
@@ -412,11 +422,20 @@ __device__ __forceinline__ void sub_hop(const SubCtx<Q> &c, int r, const double 
         // piece and every slot of a group past the chunk hold 1.0, sub_p1:
         // exact no-ops), so the product ends in group 3 -- no uniform
         // branches between the dependent multiplies
+        if (LDPC_SUB_KDISP && rc.CS < K) {  // slot K-1 holds 1.0 in every group: skip it
 #pragma unroll
-        for (int jj = 0; jj < Q; ++jj) {
+            for (int jj = 0; jj < Q; ++jj) {
 #pragma unroll
-            for (int i = 0; i < K; ++i) P = P * t[i];
-            if (jj + 1 < Q) P = group_up4(P, jj);
+                for (int i = 0; i < K - 1; ++i) P = P * t[i];
+                if (jj + 1 < Q) P = group_up4(P, jj);
+            }
+        } else {
+#pragma unroll
+            for (int jj = 0; jj < Q; ++jj) {
+#pragma unroll
+                for (int i = 0; i < K; ++i) P = P * t[i];
+                if (jj + 1 < Q) P = group_up4(P, jj);
+            }
         }
         last = Q - 1;
     } else {
