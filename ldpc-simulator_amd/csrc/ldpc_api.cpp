@@ -278,6 +278,9 @@ bool tail_vn_enabled();
 // -- the measured cross-overs; 0 = never).
 bool small_batch_cols(const DevGraph &G, int ntiles) {
     if (!G.a_packed || ((G.k + 31) >> 5) > 64 || !tail_vn_enabled()) return false;
+    // the 64-frame tile_kernel codes (wimax_576_0.5, BCH): short rows, one launch;
+    // beyond the edge path's few frames they stay on tile_kernel
+    if (ldpc::tile64_lds_bytes(G) > 0) return false;
     const char *e = getenv("LDPC_SMALL_COLS");
     const int lim = e ? atoi(e) : (G.ef == 8 ? 16 : 32);
     if (ntiles > lim) return false;
