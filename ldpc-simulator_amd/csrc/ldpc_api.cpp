@@ -895,13 +895,19 @@ bool tail_vn_enabled() {
 // 50 passes, the sub-tile kernel keeps the bulk (3/4: -2 % there;
 // profiles/r2au_tail).
 // fpw: frames per workgroup of the streaming sub-tile kernel (16, or 8 for
-// tile8_stream_kernel), one workgroup per CU.
+// tile8_stream_kernel), one workgroup per CU.  Round 4, with the
+// longest-job-first supply order: the 16-frame kernel hands off as soon as the
+// supply is out (every resident frame: 3 dB step 66.3k -> 69.1k cw/s; 3/5 of
+// them, 4,000 and "always" measured 66.3k / 68.9k / 68.6k); the 8-frame kernel,
+// whose pass is half as long, keeps 3/5 (r3/4A 3 dB: 52.3k vs 47.8k for all
+// resident) -- profiles/r4c_ab.
 int64_t handoff_frames(int64_t slots, int fpw) {
     const char *e = getenv("LDPC_HANDOFF");
     if (e) return atoll(e);
     int dev = 0, cus = 256;
     if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    return std::min<int64_t>(slots, (int64_t)cus * fpw) * 3 / 5;
+    const int64_t resident = std::min<int64_t>(slots, (int64_t)cus * fpw);
+    return fpw == 16 ? resident : resident * 3 / 5;
 }
 
 // Longest job first (frame_order.hip): the point's frames enter the slots in

@@ -275,7 +275,7 @@ __device__ __forceinline__ void t8_prefetch(const T8Ctx<K> &c, int r, T8Pre<K> &
 // 576 rows of wimax_2304_0.75A have CS = 7 of K = 8), K otherwise -- instead of
 // all K (the padded slots cost a tanh and a chain multiply each).
 #ifndef LDPC_T8_KDISP
-#define LDPC_T8_KDISP 0
+#define LDPC_T8_KDISP 2
 #endif
 template <int K, int KK, bool LA>
 __device__ __forceinline__ void t8_p1_slots(const T8Ctx<K> &c, int r, const T8Chunk &rc, const T8Pre<K> &pre,
