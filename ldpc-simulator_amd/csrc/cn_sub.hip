@@ -95,6 +95,12 @@ __global__ __launch_bounds__(64 * W, WPS) void cn_sub_kernel(DevGraph g, DevStat
     const int rs = slot % per_tile;
     const int row = rs >> 2, sub = rs & 3;
     if (tile >= st.ntiles || !st.tile_active[tile]) return;  // block-uniform, before the table staging
+    const int l64 = sub * kCsF + f;  // this lane's frame in the tile
+    const int fr = tile * kTile + l64;
+    const bool live = st.done[fr] == 0;
+    // a sub-tile whose 16 frames have all stopped (the streaming tail's
+    // compacted tiles thin out as frames finish) has nothing to store
+    if (!__syncthreads_or(live)) return;
     fill_math_lds(mlds);
     __syncthreads();
     const LdsTanh ttab{mlds.tanh};
@@ -102,9 +108,6 @@ __global__ __launch_bounds__(64 * W, WPS) void cn_sub_kernel(DevGraph g, DevStat
     const int beg = row_ptr[row], end = row_ptr[row + 1];
     const int deg = end - beg;
     if (deg == 0) return;  // spa_decoder.py:115-122
-    const int l64 = sub * kCsF + f;  // this lane's frame in the tile
-    const int fr = tile * kTile + l64;
-    const bool live = st.done[fr] == 0;
     const bool fresh = kStream && st.fresh[fr] != 0;
     double *Et = st.E + e_base(g, tile, l64);
     const double *Lt = (kFirst ? st.ch : st.L) + (size_t)tile * g.n * kTile + l64;

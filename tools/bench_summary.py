@@ -4,7 +4,8 @@ import sys
 
 d = json.loads([ln for ln in open(sys.argv[1]) if ln.startswith("{")][-1])
 r = d.get("roofline") or {}
-out = {"value": round(d["value"] or 0), "n_gpus": d.get("n_gpus"), "kernel": r.get("kernel"),
+dr = d.get("decode_roofline") or {}
+out = {"value": round(d["value"] or 0), "ms": {k[:-3]: round(v) for k, v in dr.items() if k.endswith("_ms") and v}, "n_gpus": d.get("n_gpus"), "kernel": r.get("kernel"),
        "frac": round(r.get("frac", 0), 4), "avg_launch_ms": round(r.get("avg_launch_ms", 0), 1),
        "snr_points": [(p["snr_db"], p.get("scope", "step"), round(p["value"])) for p in d.get("snr_points", [])]}
 ph = d.get("physical")
