@@ -253,17 +253,23 @@ struct T8Pre {
 #ifndef LDPC_T8_PF
 #define LDPC_T8_PF 0
 #endif
+// LDPC_FRESH_NOLOAD: a fresh streaming frame's lanes skip the E_old loads
+// (exec-masked; M = L for them), as tile_sub.hip
+#ifndef LDPC_FRESH_NOLOAD
+#define LDPC_FRESH_NOLOAD 1
+#endif
 template <int K, int I0 = 0, int I1 = K, bool kId = true>
 __device__ __forceinline__ void t8_prefetch(const T8Ctx<K> &c, int r, T8Pre<K> &p) {
     const T8Chunk rc = t8_chunk(c.row_ptr, r, c.wave);
     if (rc.cnt > 0) {  // iteration 0 forms M = L - 0.0 (== L exactly) and reads no E_old
         const uint32_t eoff = t8_eoff(c, rc);
 #pragma unroll
-        for (int i = I0; i < I1; ++i) p.eo[i] = c.first ? 0.0 : t8_ld<kNT>(c.rE, t8_es(c, eoff, i));
+        for (int i = I0; i < I1; ++i)
+            p.eo[i] = (c.first || (LDPC_FRESH_NOLOAD && c.fresh)) ? 0.0 : t8_ld<kNT>(c.rE, t8_es(c, eoff, i));
     }
     if (kId && c.wave == c.idwave && rc.deg > 0) {  // identity edge (a fresh streaming frame has L = ch: gen_slots)
         p.lid = t8_ld(c.first ? c.rC : c.rL, ((uint32_t)(c.k + r) << 9) + c.lo8);
-        p.eid = c.first ? 0.0 : t8_ld<kNT>(c.rE, ((uint32_t)(rc.beg + rc.deg - 1) << 6) + c.eo8);
+        p.eid = (c.first || (LDPC_FRESH_NOLOAD && c.fresh)) ? 0.0 : t8_ld<kNT>(c.rE, ((uint32_t)(rc.beg + rc.deg - 1) << 6) + c.eo8);
     }
 }
 

@@ -96,6 +96,12 @@ constexpr int kStaticBF = SUB_STATIC_BF;
 #define SUB_STREAM_BF 3
 #endif
 constexpr int kStreamBF = SUB_STREAM_BF;
+// LDPC_FRESH_NOLOAD (A/B, tile_sub + tile8): iteration 0 / a fresh streaming
+// frame's lanes skip the E_old loads (exec-masked) instead of loading and
+// discarding them (M = L - 0.0 == L either way).
+#ifndef LDPC_FRESH_NOLOAD
+#define LDPC_FRESH_NOLOAD 1
+#endif
 // LDPC_SUB_KDISP (A/B): rows whose pieces are shorter than K (590 of 1152 rows
 // of wimax_2304_0.5 have CS = 9 of K = 10) skip the last slot's tanh and its
 // chain multiplies (one wave-uniform branch per row) instead of padding it.
@@ -295,15 +301,16 @@ __device__ __forceinline__ bool sub_p1(const SubCtx<Q> &c, int r, const SubChunk
         const int njt = c.live ? nj : 0;  // the |t| <= 1e-10 vote: frame-less lanes abstain
         const uint16_t *lc = sub_lcols(c, r, rc);
         const uint32_t eoff = sub_eoff(c, rc);
-        // iteration 0 / a fresh streaming frame: M = L (E_old is loaded anyway
-        // and unused: L - 0.0 == L for every L)
+        // iteration 0 / a fresh streaming frame: M = L
         const bool noE = c.first || c.fresh;
         int col[K];
         double eo[K];
 #pragma unroll
         for (int i = 0; i < K; ++i) {
             if ((BF & 1) || i - i % kSG < rc.CS) {  // guarded form: every slot of a group that runs
-                eo[i] = ld_sub_msg(sub_es(c, eoff, i));
+                // a fresh frame's lane reads no E_old (LDPC_FRESH_NOLOAD: on
+                // a streaming pass most slots hold fresh frames)
+                eo[i] = (LDPC_FRESH_NOLOAD && c.fresh) ? 0.0 : ld_sub_msg(sub_es(c, eoff, i));
                 col[i] = lc[i];
             }
         }
