@@ -2,8 +2,12 @@
 """Summarize tools/profile_config4.sh into profiles/<tag>/ (committed evidence):
 kernel_stats_{sweep,static}.csv (rocprofv3 --stats) and traffic.json --
 HBM bytes from FETCH_SIZE / WRITE_SIZE (KiB), reads corrected by the gfx950
-factor re-derived on vn_kernel (profiles/r3p_final/traffic.json: 1.986;
-MI355X_MICROARCH.md: FETCH_SIZE tallies 64 B per 128-B request):
+factor calibrated on the SAME access width: the r3/4 graphs keep E in 8-frame
+blocks (64 B per lane group, as the L gather of 8 frames), and vn_kernel on
+that layout -- each message read once -- gives 1.010
+(profiles/r3b_tile8_r34_prof/summary.json); the 1.986 of the 16-frame/128-B
+layout (profiles/r3p_final, MI355X_MICROARCH.md: FETCH_SIZE tallies 64 B per
+128-B request) does not apply here:
   kernels.tile8_stream: the whole sweep (every kernel of the sweep process:
       frame order, tile8_stream_kernel, the split tail, compaction), bytes
       for the sweep -- bench.py's config4 roofline scope;
@@ -18,7 +22,7 @@ import os
 import shutil
 import sys
 
-FACTOR = 1.9860799231762316  # profiles/r3p_final/traffic.json fetch_correction_factor (vn_kernel)
+FACTOR = 1.0100041410403928  # profiles/r3b_tile8_r34_prof/summary.json (vn_kernel<false, true>, 8-frame E blocks)
 
 
 def one(path):
@@ -42,7 +46,7 @@ def bench_line(path):
 
 def main(src, dst):
     os.makedirs(dst, exist_ok=True)
-    out = {"fetch_correction_factor": FACTOR, "factor_source": "profiles/r3p_final/traffic.json (vn_kernel)",
+    out = {"fetch_correction_factor": FACTOR, "factor_source": "profiles/r3b_tile8_r34_prof/summary.json (vn_kernel on 8-frame E blocks)",
            "kernels": {}}
     for mode in ("sweep", "static"):
         st = [p for p in one(os.path.join(src, f"{mode}_trace")) if p.endswith("kernel_stats.csv")][0]
