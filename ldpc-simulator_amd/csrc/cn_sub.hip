@@ -104,7 +104,7 @@ __global__ __launch_bounds__(64 * W, WPS) void cn_sub_kernel(DevGraph g, DevStat
     fill_math_lds(mlds);
     __syncthreads();
     const LdsTanh ttab{mlds.tanh};
-    const LdsLog ltab{mlds.log};
+    const LdsAtanh ltab{mlds.atanh};
     const int beg = row_ptr[row], end = row_ptr[row + 1];
     const int deg = end - beg;
     if (deg == 0) return;  // spa_decoder.py:115-122

@@ -61,7 +61,7 @@ __global__ __launch_bounds__(256) void cn_edge_kernel(DevGraph g, DevState st, A
     fill_math_lds(mlds);
     __syncthreads();
     const LdsTanh ttab{mlds.tanh};
-    const LdsLog ltab{mlds.log};
+    const LdsAtanh ltab{mlds.atanh};
     const int lane = threadIdx.x & 63;
     const int row = (int)blockIdx.x * 4 + uniform(threadIdx.x >> 6);
     if (row >= g.m) return;

@@ -129,7 +129,7 @@ __global__ __launch_bounds__(256, LDPC_CN_WAVES) void cn_kernel(DevGraph g, DevS
     fill_math_lds(mlds);
     __syncthreads();
     const LdsTanh ttab{mlds.tanh};
-    const LdsLog ltab{mlds.log};
+    const LdsAtanh ltab{mlds.atanh};
     if (row >= g.m) return;
     const int beg = row_ptr[row], end = row_ptr[row + 1];
     if (beg == end) return;  // spa_decoder.py:115-122
@@ -234,7 +234,7 @@ __global__ __launch_bounds__(64 * W, WPS) void cn_row_kernel(DevGraph g, DevStat
     fill_math_lds(mlds);
     __syncthreads();
     const LdsTanh ttab{mlds.tanh};
-    const LdsLog ltab{mlds.log};
+    const LdsAtanh ltab{mlds.atanh};
     const int beg = row_ptr[row], end = row_ptr[row + 1];
     const int deg = end - beg;
     if (deg == 0) return;  // spa_decoder.py:115-122
@@ -325,7 +325,7 @@ __global__ __launch_bounds__(256) void cn_rare_kernel(DevGraph g, DevState st, i
     fill_math_lds(mlds);
     __syncthreads();
     const LdsTanh ttab{mlds.tanh};
-    const LdsLog ltab{mlds.log};
+    const LdsAtanh ltab{mlds.atanh};
     const int lane = threadIdx.x & 63;
     const int gw = (int)blockIdx.x * 4 + uniform(threadIdx.x >> 6);
     const int nw = (int)gridDim.x * 4;

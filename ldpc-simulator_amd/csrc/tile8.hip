@@ -184,7 +184,7 @@ struct T8Ctx {
     uint16_t *cidx;  // LDS, this wavefront's ring: row slot q, position p at [q * 16 * 8K + p]
     int *flag, *tinyf, *tseq, *p3row;
     LdsTanh ttab;
-    LdsLog ltab;
+    LdsAtanh ltab;
     AtanhCoef ac;
     int m, k, wave, j, f;
     int ep0;
@@ -632,7 +632,7 @@ __device__ __forceinline__ void t8_setup(T8Ctx<K> &c, unsigned char *lds, const 
     c.tseq = flags + 2 * kSR8;
     c.p3row = flags + 2 * kSR8 + 2;
     c.ttab = LdsTanh{mlds.tanh};
-    c.ltab = LdsLog{mlds.log};
+    c.ltab = LdsAtanh{mlds.atanh};
     c.ac = ac;
     c.m = g.m;
     c.k = g.k;

@@ -131,7 +131,7 @@ struct TileCtx {
     uint32_t *ib;      // LDS [mw][64] z^1 of the identity columns
     int *flag, *tinyf, *tseq;
     LdsTanh ttab;
-    LdsLog ltab;
+    LdsAtanh ltab;
     AtanhCoef ac;
     int k, wave;
     uint32_t lane;
@@ -410,7 +410,7 @@ __global__ __launch_bounds__(64 * kTW, 1) void tile_kernel(DevGraph g, DevState 
     c.tinyf = flags + kTR;
     c.tseq = flags + 2 * kTR;
     c.ttab = LdsTanh{mlds.tanh};
-    c.ltab = LdsLog{mlds.log};
+    c.ltab = LdsAtanh{mlds.atanh};
     c.ac = ac;
     c.k = g.k;
     c.lane = lane;
@@ -546,7 +546,7 @@ __global__ __launch_bounds__(64 * kTW, 1) void tile_stream_kernel(DevGraph g, De
     c.tinyf = flags + kTR;
     c.tseq = flags + 2 * kTR;
     c.ttab = LdsTanh{mlds.tanh};
-    c.ltab = LdsLog{mlds.log};
+    c.ltab = LdsAtanh{mlds.atanh};
     c.ac = ac;
     c.k = g.k;
     c.lane = lane;

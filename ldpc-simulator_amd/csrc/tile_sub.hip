@@ -200,7 +200,7 @@ struct SubCtx {
     int *flag, *tinyf, *tseq, *p3row;
     const int *p3dep;
     LdsTanh ttab;
-    LdsLog ltab;
+    LdsAtanh ltab;
     AtanhCoef ac;
     // uniform (SGPR) tile bases + this lane's byte offset: every access is a
     // 32-bit per-lane offset from a scalar base (global_load ... v_off, s_base)
@@ -720,7 +720,7 @@ __global__ __launch_bounds__(64 * kSW, 1) void tile_sub_kernel(DevGraph g, DevSt
     c.p3row = flags + 2 * kSR + 2;
     c.p3dep = g.p3dep;
     c.ttab = LdsTanh{mlds.tanh};
-    c.ltab = LdsLog{mlds.log};
+    c.ltab = LdsAtanh{mlds.atanh};
     c.ac = ac;
     c.k = g.k;
     c.wave = wave;
@@ -892,7 +892,7 @@ __global__ __launch_bounds__(64 * kSW, 1) void tile_sub_stream_kernel(
     c.p3row = flags + 2 * kSR + 2;
     c.p3dep = g.p3dep;
     c.ttab = LdsTanh{mlds.tanh};
-    c.ltab = LdsLog{mlds.log};
+    c.ltab = LdsAtanh{mlds.atanh};
     c.ac = ac;
     c.k = g.k;
     c.wave = wave;

@@ -58,7 +58,12 @@ def test_bench_step_counters_equal_oracle(gpu_available, snr, step, monkeypatch)
     np.testing.assert_array_equal(r.z, o["z"])
     np.testing.assert_array_equal(r.conv, o["conv"])
     np.testing.assert_array_equal(r.status, o["status"])
-    assert_llr_close(r.post, o["post"], f"posterior L at {snr} dB")
+    # frames that run all T iterations without converging (FER 3.5 % at 3 dB)
+    # can amplify one ulp of a message tens of thousands of times; where the
+    # oracle itself moves that far under one ulp of tanh, that is the bound
+    # (oracle.conditioning_slack, as tests/test_gpu_parity.py)
+    sl_L, _ = oracle.conditioning_slack(H, llr, T)
+    assert_llr_close(r.post, o["post"], f"posterior L at {snr} dB", slack=sl_L)
 
 
 def test_three_point_call_equals_oracle(gpu_available):
