@@ -869,7 +869,9 @@ def main():
         cn_name = _lib.lib().ldpc_tile_kernel_name(graph.handle).decode() or "tile_kernel"
         if args.schedule == "stream" and cn_name == "tile_kernel":
             cn_name = "tile_stream_kernel"  # the streaming Monte-Carlo variant of the same decoder
-        decode_ms = tile_ms
+        # a streamed point's last frames finish on the split path's tail (cn + vn / vn_cols
+        # launches): the whole decode's time is the tile launch's plus the tail's
+        decode_ms = tile_ms + cn_ms + vn_ms + prof.get("vn_cols", (0.0, 0))[0]
         decode_gbs = dec_bytes / (decode_ms / 1e3) / 1e9 if decode_ms else 0.0
     out = {
         "metric": METRIC,
@@ -905,7 +907,8 @@ def main():
             "bytes_model": "16 B x H_std edges x frame-iterations executed (E_old read + E_new write)",
         },
         "decode_roofline": {"achieved_GBs": decode_gbs, "frac": decode_gbs / HBM_PEAK_GBS,
-                            "cn_ms": cn_ms, "vn_ms": vn_ms, "tile_ms": tile_ms, "gen_ms": prof["generate"][0],
+                            "cn_ms": cn_ms, "vn_ms": vn_ms, "vn_cols_ms": prof.get("vn_cols", (0.0, 0))[0],
+                            "tile_ms": tile_ms, "gen_ms": prof["generate"][0],
                             "count_ms": prof["count"][0]},
         "cpu_baseline": None,
     }
@@ -949,7 +952,7 @@ def main():
             "frac": decode_gbs / HBM_PEAK_GBS, "traffic": committed_traffic(nnz, chunk, "tile")[0],
             "traffic_source": committed_traffic(nnz, chunk, "tile")[1],
             "kernel": cn_name, "launches": tile_launches, "avg_launch_ms": tile_ms / tile_launches,
-            "bytes_per_launch": dec_bytes / tile_launches,
+            "tail_ms": decode_ms - tile_ms, "bytes_per_launch": dec_bytes / tile_launches,
             "bytes_model": "per frame 8 n (channel LLRs) + 16 B x H_std edges x iterations executed "
                            "(E_old read + E_new write) + ceil(n/8) + 8 (SURVEY 8d); CN and VN fused",
         }
