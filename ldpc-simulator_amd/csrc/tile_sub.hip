@@ -108,6 +108,15 @@ constexpr int kStreamBF = SUB_STREAM_BF;
 #ifndef LDPC_SUB_KDISP
 #define LDPC_SUB_KDISP 0
 #endif
+// Timing experiments only (WRONG values by construction, never in a shipped
+// build): LDPC_EXP_NOEOLD drops every E_old load (M = L), LDPC_EXP_NOEST drops
+// every E_new store -- what the message stream costs (profiles/r4o_msg).
+#ifndef LDPC_EXP_NOEOLD
+#define LDPC_EXP_NOEOLD 0
+#endif
+#ifndef LDPC_EXP_NOEST
+#define LDPC_EXP_NOEST 0
+#endif
 // the branch-free hop (Q = 4) multiplies all K slots: P1 must pad them (bit 0)
 static_assert(((kStaticBF & kStreamBF) & 1) != 0, "the branch-free hop needs the branch-free P1");
 // Logical wavefront (chunk position in a row) of hardware wavefront hw: the
@@ -310,7 +319,7 @@ __device__ __forceinline__ bool sub_p1(const SubCtx<Q> &c, int r, const SubChunk
             if ((BF & 1) || i - i % kSG < rc.CS) {  // guarded form: every slot of a group that runs
                 // a fresh frame's lane reads no E_old (LDPC_FRESH_NOLOAD: on
                 // a streaming pass most slots hold fresh frames)
-                eo[i] = (LDPC_FRESH_NOLOAD && c.fresh) ? 0.0 : ld_sub_msg(sub_es(c, eoff, i));
+                eo[i] = (LDPC_EXP_NOEOLD || (LDPC_FRESH_NOLOAD && c.fresh)) ? 0.0 : ld_sub_msg(sub_es(c, eoff, i));
                 col[i] = lc[i];
             }
         }
@@ -561,7 +570,7 @@ __device__ __forceinline__ void sub_p3_body(SubCtx<Q> &c, int r, double (&t)[Sub
             }
         }
     }
-    if (c.live) {
+    if (c.live && !LDPC_EXP_NOEST) {
         const uint32_t eoff = sub_eoff(c, rc);
 #pragma unroll
         for (int i = 0; i < K; ++i)
