@@ -283,7 +283,24 @@ __device__ __forceinline__ void t8_prefetch(const T8Ctx<K> &c, int r, T8Pre<K> &
 #ifndef LDPC_T8_KDISP
 #define LDPC_T8_KDISP 2
 #endif
-template <int K, int KK, bool LA>
+// LDPC_T8_SATMEMO: P3 reuses slot 0's E_new for the slots whose quotients all
+// have slot 0's magnitude (t8_p3; saturated rows: config 4's 3.5 / 4 dB points,
+// +23 % there, -0.7 % at 1 dB, profiles/r4w_ab)
+#ifndef LDPC_T8_SATMEMO
+#define LDPC_T8_SATMEMO 1
+#endif
+// The P1 half (LDPC_T8_SATP1=1, A/B, not the default): a pass flagged
+// saturated by t8_sat_next runs a P1 form that gives a slot t = +-CL without
+// the tanh polynomial where every lane's |M| >= 35.  profiles/r4w_ab: +9 % at
+// 3.5 dB alone, but -4.5 % at 1 dB (the second row-loop copy doubles the
+// kernel's code) and less than the P3 half with it (7,026 vs 6,838 cw/s)
+#ifndef LDPC_T8_SATP1
+#define LDPC_T8_SATP1 0
+#endif
+#ifndef LDPC_T8_SATP3  // A/B: the P3 half alone
+#define LDPC_T8_SATP3 LDPC_T8_SATMEMO
+#endif
+template <int K, int KK, bool LA, bool SAT>
 __device__ __forceinline__ void t8_p1_slots(const T8Ctx<K> &c, int r, const T8Chunk &rc, const T8Pre<K> &pre,
                                             double (&t)[K], bool &tiny, bool skip_last = false) {
     const int nj = t8_nj(c, rc);
@@ -301,33 +318,55 @@ __device__ __forceinline__ void t8_p1_slots(const T8Ctx<K> &c, int r, const T8Ch
 #pragma unroll
         for (int i = 0; i < KK; ++i) Lv[i] = t8_ld(rs, ((uint32_t)col[i] << 9) + c.lo8);
     }
+    // Slots saturated in every lane that matters (|M| >= 35: d = M/2 is
+    // clipped to +-17.5, t = +-np.tanh(17.5) = +-CL, tests/test_math.py) need
+    // no tanh polynomial -- config 4's 3.5 / 4 dB points, where 99.8 % of the
+    // edges saturate.  Only passes flagged saturated (t8_sat_next) run this
+    // form: its per-slot branches cost the other passes their cross-slot overlap.
+    if constexpr (!SAT) {
 #pragma unroll
-    for (int i = 0; i < KK; ++i) {
-        if (i == KK - 1 && skip_last) {  // wave-uniform: no piece reaches slot K-1 in this row
-            t[i] = 1.0;
-            continue;
+        for (int i = 0; i < KK; ++i) {
+            if (i == KK - 1 && skip_last) {  // wave-uniform: no piece reaches slot K-1 in this row
+                t[i] = 1.0;
+                continue;
+            }
+            // :85-90 / :260-268 (eo = 0.0 on iteration 0; a fresh streaming frame M = L)
+            const double M = c.fresh ? Lv[i] : Lv[i] - pre.eo[i];
+            const double tv = tanh_half_clipped(M, c.ttab);  // :138-146 (spa_math.h)
+            tiny |= i < njt && !(fabs(tv) > kTiny);
+            t[i] = i < nj ? tv : 1.0;  // past the piece: an exact no-op in the product
+            t8_slot_fence();
         }
-        // :85-90 / :260-268 (eo = 0.0 on iteration 0; a fresh streaming frame M = L)
-        const double M = c.fresh ? Lv[i] : Lv[i] - pre.eo[i];
-        const double tv = tanh_half_clipped(M, c.ttab);  // :138-146 (spa_math.h)
-        tiny |= i < njt && !(fabs(tv) > kTiny);
-        t[i] = i < nj ? tv : 1.0;  // past the piece: an exact no-op in the product
-        t8_slot_fence();
+    } else {
+#pragma unroll
+        for (int i = 0; i < KK; ++i) {
+            if (i == KK - 1 && skip_last) {
+                t[i] = 1.0;
+                continue;
+            }
+            const double M = c.fresh ? Lv[i] : Lv[i] - pre.eo[i];
+            const double tv = __ballot(i < njt && !(fabs(M) >= 35.0)) == 0ull
+                                  ? dfrom(dbits(kCL) | (dbits(M) & 0x8000000000000000ull))
+                                  : tanh_half_clipped(M, c.ttab);
+            tiny |= i < njt && !(fabs(tv) > kTiny);
+            t[i] = i < nj ? tv : 1.0;
+            t8_slot_fence();
+        }
     }
 #pragma unroll
     for (int i = KK; i < K; ++i) t[i] = 1.0;
 }
 
-template <int K, bool LA>
+template <int K, bool LA, bool SAT>
 __device__ __forceinline__ bool t8_p1(const T8Ctx<K> &c, int r, const T8Pre<K> &pre, double (&t)[K]) {
     bool tiny = false;
     const int sv = t8_stage_issue(c, r + 1);
     const T8Chunk rc = t8_chunk(c.row_ptr, r, c.wave);
     if (rc.cnt > 0) {
         if (LDPC_T8_KDISP == 1 && K > 1 && rc.CS < K)
-            t8_p1_slots<K, (K > 1 ? K - 1 : K), LA>(c, r, rc, pre, t, tiny);
+            t8_p1_slots<K, (K > 1 ? K - 1 : K), LA, SAT>(c, r, rc, pre, t, tiny);
         else
-            t8_p1_slots<K, K, LA>(c, r, rc, pre, t, tiny, LDPC_T8_KDISP == 2 && rc.CS < K);
+            t8_p1_slots<K, K, LA, SAT>(c, r, rc, pre, t, tiny, LDPC_T8_KDISP == 2 && rc.CS < K);
     } else {
 #pragma unroll
         for (int i = 0; i < K; ++i) t[i] = 1.0;
@@ -458,10 +497,38 @@ __device__ __forceinline__ void t8_p3(T8Ctx<K> &c, int r, double (&t)[K]) {
         };
         if (div_nr_ok(c.live ? P : 1.0)) {  // the IEEE quotient without its scaling steps (cn_common.h)
             if (rc.cnt > 0) {
+                if (LDPC_T8_SATP3 && K == 8) {  // the r3/4 form (the L_A form spills with it)
+                    // Saturated rows (config 4's 3.5 and 4 dB points: 99.8 % of
+                    // the edges have |M| >= 35, t = +-CL) give most slots one
+                    // quotient magnitude.  atanh_f(clip_cl(q)) is odd in q and
+                    // 2q == 2 atanh_f(clip_cl(q)) below 2^-27, so a slot where
+                    // every lane's |q| equals its slot-0 |q| takes slot 0's
+                    // E_new with its own sign: the same function of the same
+                    // argument (bit for bit; the key only decides how often it
+                    // hits), one atanh per lane and row instead of one per slot.
+                    // Lanes that do not vote (frame-less, past the piece) keep
+                    // values nothing stores or uses.
+                    double key = 0.0;
 #pragma unroll
-                for (int i = 0; i < K; ++i) {
-                    if (i < rc.CS) t[i] = en(div_nr(P, t[i]));
-                    t8_slot_fence();
+                    for (int i = 0; i < K; ++i) {
+                        if (i < rc.CS) {
+                            const double q = div_nr(P, t[i]);
+                            if (i == 0) key = fabs(q);
+                            if (__ballot(!(fabs(q) < lim)) == 0ull)
+                                t[i] = 2.0 * q;
+                            else if (i > 0 && __ballot(c.live && i < nj && fabs(q) != key) == 0ull)
+                                t[i] = dfrom((dbits(t[0]) & 0x7fffffffffffffffull) | (dbits(q) & 0x8000000000000000ull));
+                            else
+                                t[i] = 2.0 * atanh_f(clip_cl(q), c.ltab, c.ac);
+                        }
+                        t8_slot_fence();
+                    }
+                } else {
+#pragma unroll
+                    for (int i = 0; i < K; ++i) {
+                        if (i < rc.CS) t[i] = en(div_nr(P, t[i]));
+                        t8_slot_fence();
+                    }
                 }
             }
             if (idw) EI = en(div_nr(P, tI));
@@ -560,7 +627,7 @@ __device__ __forceinline__ void t8_p3(T8Ctx<K> &c, int r, double (&t)[K]) {
 // LA variants prefetch the next row's E_old (and identity loads) before
 // hop + P3; the L-gathering variant (8 slots per lane) has no registers for
 // that and issues them at the start of P1.
-template <int K, bool LA, int D, int B>
+template <int K, bool LA, int D, int B, bool SAT>
 __device__ __forceinline__ void t8_body(T8Ctx<K> &c, int r, double (&t)[D][K], bool (&y)[D]) {
     constexpr int N = (B + 1) % D;
     T8Pre<K> pre;
@@ -573,13 +640,13 @@ __device__ __forceinline__ void t8_body(T8Ctx<K> &c, int r, double (&t)[D][K], b
     if (r >= D - 1) t8_p3(c, r - (D - 1), t[N]);
     T8_STAMP(a2);
     if (!LA && r + 1 < c.m) t8_prefetch<K, (LDPC_T8_PF < K ? LDPC_T8_PF : K), K, true>(c, r + 1, pre);
-    if (r + 1 < c.m) y[N] = t8_p1<K, LA>(c, r + 1, pre, t[N]);
+    if (r + 1 < c.m) y[N] = t8_p1<K, LA, SAT>(c, r + 1, pre, t[N]);
     T8_STAMP(a3);
     T8_ADD(c, 6, a2, a3);
 }
 
 // One pass over all rows (every P3 done on return, before the barrier).
-template <int K, bool LA, int D>
+template <int K, bool LA, int D, bool SAT>
 __device__ __forceinline__ void t8_rows(T8Ctx<K> &c) {
     const int m = c.m;
     double t[D][K];
@@ -589,14 +656,14 @@ __device__ __forceinline__ void t8_rows(T8Ctx<K> &c) {
         t8_stage_commit(c, 0, t8_stage_issue(c, 0));
         T8Pre<K> pre;
         t8_prefetch(c, 0, pre);
-        y[0] = t8_p1<K, LA>(c, 0, pre, t[0]);
+        y[0] = t8_p1<K, LA, SAT>(c, 0, pre, t[0]);
     }
     const int last = m + D - 2;  // body(last) runs P3(m-1)
     for (int r = 0; r <= last; r += D) {
-        t8_body<K, LA, D, 0>(c, r, t, y);
-        if (r + 1 <= last) t8_body<K, LA, D, 1>(c, r + 1, t, y);
+        t8_body<K, LA, D, 0, SAT>(c, r, t, y);
+        if (r + 1 <= last) t8_body<K, LA, D, 1, SAT>(c, r + 1, t, y);
         if constexpr (D == 3)
-            if (r + 2 <= last) t8_body<K, LA, D, 2>(c, r + 2, t, y);
+            if (r + 2 <= last) t8_body<K, LA, D, 2, SAT>(c, r + 2, t, y);
     }
 }
 
@@ -656,12 +723,13 @@ __device__ __forceinline__ int t8_epoch0(int pass, int m) {
 template <bool LA>
 __device__ __forceinline__ void t8_vn(const DevGraph &g, double *S, double *LAl, uint32_t *zb, int *cntl,
                                       const int *livel, __amdgpu_buffer_rsrc_t rL, __amdgpu_buffer_rsrc_t rC,
-                                      int sub, bool first, bool fresh_any, const int *freshl, int nllr) {
+                                      int sub, bool first, bool fresh_any, const int *freshl, int nllr,
+                                      int *satc) {
     const int ff = threadIdx.x & 7;
     const uint32_t lo8 = (uint32_t)(sub * kF8 + ff) * 8u;
     const bool live = livel[ff] != 0;
     const bool fr = fresh_any && freshl[ff] != 0;
-    int my_cnt = 0;
+    int my_cnt = 0, my_sat = 0;
     for (int e = threadIdx.x; e < g.k * kF8; e += blockDim.x) {
         const int col = e >> 3;
         const double Sj = S[e];
@@ -679,10 +747,17 @@ __device__ __forceinline__ void t8_vn(const DevGraph &g, double *S, double *LAl,
             my_cnt += (fabs(Lj) <= 7.0 && ap * Lj < 0.0) ? 1 : 0;
         }
         if (LA) LAl[e] = Lj;
+        my_sat += live && fabs(Lj) >= 35.0 ? 1 : 0;
         if (live) t8_st(rL, ((uint32_t)col << 9) + lo8, Lj);
         if (!(Lj < 0.0)) atomicOr(zb + (col >> 5) * kF8 + ff, 1u << (col & 31));
     }
     if (nllr && my_cnt) atomicAdd(cntl + ff, my_cnt);
+    if (LDPC_T8_SATP1 && my_sat) atomicAdd(satc, my_sat);
+}
+// The next pass tests P1's slots for saturation when >= 95 % of the 8 frames'
+// A posteriors have |L| >= 35 (a heuristic: both P1 forms are exact)
+__device__ __forceinline__ bool t8_sat_next(const DevGraph &g, const int *satc) {
+    return LDPC_T8_SATP1 && (long long)*satc * 20 >= (long long)g.k * kF8 * 19;
 }
 
 // syndrome (:191-204): parity of row r = popcount(A_r & (z^1)_A) + (z^1)_{k+r}
@@ -750,20 +825,28 @@ __global__ __launch_bounds__(64 * kW8, 1) void tile8_kernel(DevGraph g, DevState
     c.idwave = D >= 3 ? 0 : kW8 - 1;
     const int fr = tile * kTile + sub * kF8 + c.f;  // this lane's frame
 
+    __shared__ int satc;  // saturated A posteriors of the last pass (t8_vn)
+    if (threadIdx.x == 0) satc = 0;
+    bool satn = false;
     for (int it = 0; it < max_iter; ++it) {
         c.first = it == 0;
         c.live = livel[c.f] != 0;
         c.ep0 = t8_epoch0(it, g.m);
         T8_STAMP(w0);
-        t8_rows<K, LA, D>(c);
+        if (!LA && LDPC_T8_SATP1 && satn)  // wave-uniform (LDS count): one form per pass
+            t8_rows<K, LA, D, true>(c);
+        else
+            t8_rows<K, LA, D, false>(c);
         T8_STAMP(w1);
         T8_ADD(c, 8, w0, w1);
         __syncthreads();  // every P3 done: S complete, identity bits set
         if (threadIdx.x < kW8) c.p3row[threadIdx.x] = 0;
-        t8_vn<LA>(g, S, LAl, zb, cntl, livel, rL, rC, sub, c.first, false, nullptr, nllr);
+        t8_vn<LA>(g, S, LAl, zb, cntl, livel, rL, rC, sub, c.first, false, nullptr, nllr, &satc);
         __syncthreads();
+        satn = t8_sat_next(g, &satc);
         t8_syndrome(g, zb, ib, bad);
         __syncthreads();
+        if (threadIdx.x == 0) satc = 0;  // read by every thread before the barrier above
         if ((threadIdx.x >> 6) == 0) {  // per-frame exits, as vn_kernel (static schedule)
             bool still = false;
             if (lane < kF8 && livel[lane] != 0) {
@@ -831,6 +914,7 @@ __global__ __launch_bounds__(64 * kW8, 1) void tile8_stream_kernel(
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     __shared__ long long gidx[kF8];  // refill: slot f's new frame index (< 0: none)
     __shared__ int nref;             // refill: some slot took a frame this pass
+    __shared__ int satc;             // saturated A posteriors of the last pass (t8_vn)
     const T8Layout ly = t8_layout(g.k, g.m, K, LA, D + 1);
     double *S = (double *)(lds + ly.S);
     double *LAl = LA ? (double *)(lds + ly.LA) : nullptr;
@@ -866,6 +950,8 @@ __global__ __launch_bounds__(64 * kW8, 1) void tile8_stream_kernel(
     const int m = g.m;
     const uint32_t *Ut = st.ubits + (size_t)tile * kw * kTile + sub * kF8 + lane;  // slot lanes only
 
+    if (threadIdx.x == 0) satc = 0;  // ordered before t8_vn's adds by the pass's barriers
+    bool satn = false;
     for (int pass = 0;; ++pass) {
         __syncthreads();  // the previous pass's exits (or the set-up) are visible
         if (w0) {  // refill: slots without a frame take the next indices
@@ -926,13 +1012,18 @@ __global__ __launch_bounds__(64 * kW8, 1) void tile8_stream_kernel(
         c.fresh = freshl[c.f] != 0;
         c.first = false;
         c.ep0 = t8_epoch0(pass, m);
-        t8_rows<K, LA, D>(c);
+        if (!LA && LDPC_T8_SATP1 && satn)  // wave-uniform (LDS count): one form per pass
+            t8_rows<K, LA, D, true>(c);
+        else
+            t8_rows<K, LA, D, false>(c);
         __syncthreads();  // every P3 done: S complete, identity bits set
         if (threadIdx.x < kW8) c.p3row[threadIdx.x] = 0;
-        t8_vn<LA>(g, S, LAl, zb, cntl, livel, rL, rC, sub, false, true, freshl, nllr);
+        t8_vn<LA>(g, S, LAl, zb, cntl, livel, rL, rC, sub, false, true, freshl, nllr, &satc);
         __syncthreads();
+        satn = t8_sat_next(g, &satc);
         t8_syndrome(g, zb, ib, bad);
         __syncthreads();
+        if (threadIdx.x == 0) satc = 0;
         if (w0) {  // per-slot exits and counters (vn_kernel's stream variant)
             unsigned long long cv[7] = {0, 0, 0, 0, 0, 0, 0};
             bool fin = false;
@@ -985,7 +1076,7 @@ size_t t8_lds_bytes_k(const DevGraph &g) {
     const int C = (g.max_row_deg + kW8 - 1) / kW8;
     if ((C + kQ8 - 1) / kQ8 > K) return 0;
     const size_t b = t8_layout(g.k, g.m, K, LA, D + 1).total;
-    return b <= kLds8Max ? b : 0;
+    return b + 16 <= kLds8Max ? b : 0;  // + the static __shared__ counter(s)
 }
 
 // the variant a graph runs: 0 = none, else K * 2 + LA

@@ -154,3 +154,20 @@ def test_atanh_is_identity_below_2_pow_minus_27(host_math):
     np.testing.assert_array_equal(y.view(np.int64), q.view(np.int64))
     w = rng.uniform(2.0 ** -26, 2.0 ** -25, 100_000)
     assert (_run(host_math.host_atanh, w) != w).any()
+
+
+def test_atanh_is_odd_for_the_saturation_memo(host_math):
+    """tile8.hip t8_p3 (LDPC_T8_SATMEMO) gives a slot whose every lane has
+    |q| == |q of slot 0| slot 0's E_new with the slot's own sign.  That is
+    exact iff E(q) = 2 atanh_f(clip_cl(q)) is odd bit for bit (clip_cl is
+    fmin/fmax: symmetric) -- and, where slot 0 took the 2q branch (every
+    |q| < 2^-27), iff atanh_f(q) == q there (asserted last)."""
+    rng = np.random.default_rng(11)
+    q = np.concatenate([rng.uniform(0, CL, 400_000), 10.0 ** rng.uniform(-300, 0, 200_000),
+                        CL - rng.uniform(0, 1e-12, 1000), [CL, 0.0, 2.0 ** -27, 2.0 ** -5, 0.5]])
+    q = np.minimum(q, CL)
+    pos = _run(host_math.host_atanh, q)
+    neg = _run(host_math.host_atanh, -q)
+    assert np.array_equal(neg.view(np.uint64), (-pos).view(np.uint64))
+    small = q[q < 2.0 ** -27]
+    assert np.array_equal(_run(host_math.host_atanh, small), small)
