@@ -146,7 +146,10 @@ def test_tile8_is_the_one_launched(gpu_available, monkeypatch):
 @pytest.mark.parametrize("code,snr,T,B", [("wimax_2304_0.5", 0.0, 4, 70), ("wimax_2304_0.5", 3.0, 25, 40),
                                           ("wimax_2304_0.5", 1.0, 50, 64),
                                           ("wimax_2304_0.75A", 2.0, 5, 64), ("wimax_2304_0.75A", 1.0, 30, 72),
-                                          ("wimax_2304_0.75B", 4.0, 8, 24)])
+                                          ("wimax_2304_0.75B", 4.0, 8, 24),
+                                          # saturated rows (config 4's 3.5 / 4 dB: tile8's P3 memo,
+                                          # LDPC_T8_SATMEMO) against the split path's per-edge atanh
+                                          ("wimax_2304_0.75A", 4.0, 50, 72), ("wimax_2304_0.75A", 3.5, 20, 64)])
 def test_tile8_bit_identical_to_split(gpu_available, monkeypatch, code, snr, T, B):
     llr = _random_llr(hstd_for(code), B, snr, seed=int(100 * snr) + 2000 + T)
     dec = _t8(code, B, monkeypatch)
