@@ -105,8 +105,8 @@ namespace {
 // wavefront waits for all 16 (whose in-order P3s then cover every row before).
 // drop_last: chunk all but each row's last edge (tile8.hip: the identity
 // column k + r of an [A | I_m] row is wavefront 0's, outside the chunks).
+template <int W = ldpc::kSubWaves>
 std::vector<int> sub_p3_deps(int m, const int *row_ptr, const int *col_idx, bool drop_last = false) {
-    constexpr int W = ldpc::kSubWaves;
     std::vector<int> dep((size_t)m * W, 1);  // lo 1 > hi 0: no wait
     auto spans = [&](int r, long long lo[W], long long hi[W], bool ne[W]) {
         const int beg = row_ptr[r];
@@ -497,7 +497,9 @@ int ldpc_graph_create(int32_t m, int32_t n, const int32_t *row_ptr, const int32_
     if (device < 0) (void)hipGetDevice(&g->device);
     const std::vector<int> p3dep = sub_p3_deps(m, row_ptr, col_idx);
     const std::vector<int> p3dep8 = sub_p3_deps(m, row_ptr, col_idx, true);
-    const size_t nints = (size_t)(m + 1) + nnz + (size_t)(n + 1) + 2 * (size_t)nnz + p3dep.size() + p3dep8.size();
+    const std::vector<int> p3dep12 = sub_p3_deps<12>(m, row_ptr, col_idx);
+    const size_t nints = (size_t)(m + 1) + nnz + (size_t)(n + 1) + 2 * (size_t)nnz + p3dep.size() + p3dep8.size() +
+                         p3dep12.size();
     if (int rc = dev_alloc(&g->d_ints, nints)) {
         delete g;
         return rc;
@@ -526,6 +528,8 @@ int ldpc_graph_create(int32_t m, int32_t n, const int32_t *row_ptr, const int32_
     G.p3dep = p;
     p += p3dep.size();
     G.p3dep8 = p;
+    p += p3dep8.size();
+    G.p3dep12 = p;
     hipError_t e = hipSuccess;
     if (e == hipSuccess) e = hipMemcpy((void *)G.row_ptr, row_ptr, sizeof(int) * (m + 1), hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMemcpy((void *)G.col_idx, col_idx, sizeof(int) * nnz, hipMemcpyHostToDevice);
@@ -536,6 +540,8 @@ int ldpc_graph_create(int32_t m, int32_t n, const int32_t *row_ptr, const int32_
         e = hipMemcpy((void *)G.p3dep, p3dep.data(), sizeof(int) * p3dep.size(), hipMemcpyHostToDevice);
     if (e == hipSuccess && m > 0)
         e = hipMemcpy((void *)G.p3dep8, p3dep8.data(), sizeof(int) * p3dep8.size(), hipMemcpyHostToDevice);
+    if (e == hipSuccess && m > 0)
+        e = hipMemcpy((void *)G.p3dep12, p3dep12.data(), sizeof(int) * p3dep12.size(), hipMemcpyHostToDevice);
     if (e == hipSuccess && std_form && k > 0) {  // encoder table: A bit-packed per row
         const size_t kw = (size_t)(k + 31) / 32;
         std::vector<uint32_t> ap((size_t)m * kw, 0u);

@@ -51,13 +51,22 @@
 namespace ldpc {
 namespace {
 
-constexpr int kSW = kSubWaves;          // wavefronts per workgroup (spa_device.h)
+// wavefronts per workgroup: kSubWaves (16, spa_device.h); LDPC_SUB_WAVES=12
+// (A/B): 3 wavefronts per SIMD with 168 registers each, K = 14 slots per lane
+// (the P3 order table DevGraph::p3dep12): 18 instead of 28 spilled VGPRs, but
+// 0.426 vs 0.452 of HBM at 1 dB (profiles/r4z_ab) -- the fourth wavefront per
+// SIMD hides more latency than the spills cost
+#ifndef LDPC_SUB_WAVES
+#define LDPC_SUB_WAVES 16
+#endif
+constexpr int kSW = LDPC_SUB_WAVES;
+static_assert(kSW == kSubWaves || kSW == 12, "P3 order tables exist for 16 and 12 wavefronts (16 x 64 = the workgroup limit)");
 constexpr size_t kSubLdsMax = 163840;
 
 template <int Q>
 struct SubCfg {
     static constexpr int F = kTile / Q;           // frames per workgroup
-    static constexpr int K = Q == 4 ? 10 : 8;     // slots per lane: row degree <= kSW * Q * K
+    static constexpr int K = Q == 4 ? (kSW == 12 ? 14 : 10) : 8;  // slots per lane: row degree <= kSW * Q * K
 };
 
 // The product crosses lane groups by v_permlane16/32_swap (Q = 4) or
@@ -125,7 +134,7 @@ static_assert(((kStaticBF & kStreamBF) & 1) != 0, "the branch-free hop needs the
 // chain and its P3 neighbours.  +1.3 % over the identity map, static and
 // streaming (profiles/r2at_wave_map; pairs of positions per SIMD measured the
 // same, spin waits at a lower issue priority +0.2 %).
-__device__ __forceinline__ int sub_wave(int hw) { return (hw & 3) * 4 + (hw >> 2); }
+__device__ __forceinline__ int sub_wave(int hw) { return (hw & 3) * (kSW / 4) + (hw >> 2); }
 __device__ __forceinline__ double ld_sub_msg(const double *p) { return __builtin_nontemporal_load(p); }
 // LDPC_EST_SC1 (A/B): E_new stored sc1 (the line is written through and
 // dropped from the XCD's L2, MI355X_MICROARCH.md: nt and plain stores keep it,
@@ -727,7 +736,7 @@ __global__ __launch_bounds__(64 * kSW, 1) void tile_sub_kernel(DevGraph g, DevSt
     c.tinyf = flags + kSR;
     c.tseq = flags + 2 * kSR;
     c.p3row = flags + 2 * kSR + 2;
-    c.p3dep = g.p3dep;
+    c.p3dep = kSW == 12 ? g.p3dep12 : g.p3dep;
     c.ttab = LdsTanh{mlds.tanh};
     c.ltab = LdsAtanh{mlds.atanh};
     c.ac = ac;
@@ -899,7 +908,7 @@ __global__ __launch_bounds__(64 * kSW, 1) void tile_sub_stream_kernel(
     c.tinyf = flags + kSR;
     c.tseq = flags + 2 * kSR;
     c.p3row = flags + 2 * kSR + 2;
-    c.p3dep = g.p3dep;
+    c.p3dep = kSW == 12 ? g.p3dep12 : g.p3dep;
     c.ttab = LdsTanh{mlds.tanh};
     c.ltab = LdsAtanh{mlds.atanh};
     c.ac = ac;
