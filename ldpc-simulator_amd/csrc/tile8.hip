@@ -283,6 +283,11 @@ __device__ __forceinline__ void t8_prefetch(const T8Ctx<K> &c, int r, T8Pre<K> &
 #ifndef LDPC_T8_KDISP
 #define LDPC_T8_KDISP 2
 #endif
+// LDPC_T8_LDSADD: P3's column-sum updates as ds_add_f64 (as tile_sub.hip's
+// LDPC_SUB_LDSADD: the same IEEE adds in the same order, no read round trip)
+#ifndef LDPC_T8_LDSADD
+#define LDPC_T8_LDSADD 1
+#endif
 // LDPC_T8_SATMEMO: P3 reuses slot 0's E_new for the slots whose quotients all
 // have slot 0's magnitude (t8_p3; saturated rows: config 4's 3.5 / 4 dB points,
 // +23 % there, -0.7 % at 1 dB, profiles/r4w_ab)
@@ -605,12 +610,17 @@ __device__ __forceinline__ void t8_p3(T8Ctx<K> &c, int r, double (&t)[K]) {
         double sv[K];
 #pragma unroll
         for (int i = 0; i < K; ++i) sp[i] = i < nj ? c.S + (size_t)col[i] * kF8 : c.dummy;
+        if (LDPC_T8_LDSADD) {  // one ds_add_f64 per slot (tile_sub.hip LDPC_SUB_LDSADD); past the piece: `dummy`
 #pragma unroll
-        for (int i = 0; i < K; ++i) sv[i] = *sp[i];
+            for (int i = 0; i < K; ++i) __hip_atomic_fetch_add(sp[i], t[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        } else {
 #pragma unroll
-        for (int i = 0; i < K; ++i) sv[i] = sv[i] + t[i];
+            for (int i = 0; i < K; ++i) sv[i] = *sp[i];
 #pragma unroll
-        for (int i = 0; i < K; ++i) *sp[i] = sv[i];
+            for (int i = 0; i < K; ++i) sv[i] = sv[i] + t[i];
+#pragma unroll
+            for (int i = 0; i < K; ++i) *sp[i] = sv[i];
+        }
     }
     if (idw && c.j == 0) {  // identity column: L = ch + (0 + E) (:173-185)
         const double Lj = chI + (0.0 + EI);

@@ -117,6 +117,15 @@ constexpr int kStreamBF = SUB_STREAM_BF;
 #ifndef LDPC_SUB_KDISP
 #define LDPC_SUB_KDISP 0
 #endif
+// LDPC_SUB_LDSADD: P3's column-sum updates as ds_add_f64 instead of read /
+// add / write (one LDS op per slot, no read round trip; +2 % at 1 dB,
+// profiles/r4za_ab).  The same IEEE add of the same operands in the same order
+// (the p3dep waits order a column's additions): ds_add_f64 rounds to nearest
+// even and, unlike the other LDS float atomics, never flushes denormals
+// (LLVM SIISelLowering emits it for workgroup-scope fadd only on that basis)
+#ifndef LDPC_SUB_LDSADD
+#define LDPC_SUB_LDSADD 1
+#endif
 // Timing experiments only (WRONG values by construction, never in a shipped
 // build): LDPC_EXP_NOEOLD drops every E_old load (M = L), LDPC_EXP_NOEST drops
 // every E_new store -- what the message stream costs (profiles/r4o_msg).
@@ -602,12 +611,18 @@ __device__ __forceinline__ void sub_p3_body(SubCtx<Q> &c, int r, double (&t)[Sub
                 colI = col[i];
             }
         }
+        if (LDPC_SUB_LDSADD) {  // A/B: one LDS fp64 atomic add per slot, no read round trip
 #pragma unroll
-        for (int i = 0; i < K; ++i) sv[i] = *sp[i];
+            for (int i = 0; i < K; ++i)  // slots past the piece add into `dummy` (never read)
+                __hip_atomic_fetch_add(sp[i], t[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        } else {
 #pragma unroll
-        for (int i = 0; i < K; ++i) sv[i] = sv[i] + t[i];
+            for (int i = 0; i < K; ++i) sv[i] = *sp[i];
 #pragma unroll
-        for (int i = 0; i < K; ++i) *sp[i] = sv[i];
+            for (int i = 0; i < K; ++i) sv[i] = sv[i] + t[i];
+#pragma unroll
+            for (int i = 0; i < K; ++i) *sp[i] = sv[i];
+        }
     } else {
 #pragma unroll
         for (int i = 0; i < K; ++i) {
