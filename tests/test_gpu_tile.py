@@ -242,3 +242,23 @@ def test_cn_sub_stream_counters(gpu_available, monkeypatch):
     monkeypatch.setenv("LDPC_CN_SUB", "0")
     b = dec.mc_run(20260213, sig, 900, 33, 20, nllr=True, split=True)
     np.testing.assert_array_equal(a, b)
+
+
+@pytest.mark.parametrize("code,lo,hi", [("wimax_576_0.5", 0.011, 0.015),     # tile_kernel
+                                        ("wimax_2304_0.5", 0.5, 0.7),         # tile_sub_kernel<4>
+                                        ("wimax_2304_0.75A", 0.85, 1.05)])    # tile8_kernel
+def test_subnormal_column_sums_identical(gpu_available, code, lo, hi):
+    """The tile decoders add E_new into the LDS column sums with ds_add_f64
+    (LDPC_*_LDSADD); the split path adds with v_add_f64 in vn_kernel.  LLR
+    magnitudes chosen so the row products underflow: ~28-50 % of the messages
+    are subnormal (checked below), so a flushing add would show."""
+    H = hstd_for(code)
+    rng = np.random.default_rng(5)
+    B = 70
+    llr = rng.uniform(lo, hi, (B, H.shape[1])) * rng.choice([-1.0, 1.0], (B, H.shape[1]))
+    dec = _decoder(code, B)
+    a = dec.decode(llr, 2, nllr=True, post=True, hist=True, msgs=True)
+    b = dec.decode(llr, 2, nllr=True, post=True, hist=True, msgs=True, split=True)
+    sub = (a.msgs != 0) & (np.abs(a.msgs) < np.finfo(np.float64).tiny)
+    assert sub.mean() > 0.2, sub.mean()
+    _assert_identical(a, b)
