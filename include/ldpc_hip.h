@@ -85,9 +85,12 @@ void ldpc_hstd_free(ldpc_hstd *h);
 int ldpc_graph_create(int32_t m, int32_t n, const int32_t *row_ptr, const int32_t *col_idx,
                       int32_t device, ldpc_graph **out);
 int ldpc_graph_destroy(ldpc_graph *g);
-/* Name of the check-node kernel the parity decoder launches for this graph
- * ("cn_row_kernel": rows of degree <= 192 kept in registers, 16 B/edge;
- * "cn_kernel": one wavefront per row, 24 B/edge) -- measurement labels. */
+/* Name of the check-node kernel the split parity path launches for this graph
+ * on large batches ("cn_row_kernel": rows of degree <= 192 kept in registers,
+ * 16 B/edge; "cn_kernel": one wavefront per row, 24 B/edge) -- measurement
+ * labels.  Batches of <= 128 tiles of the 2304 codes (the streaming tail,
+ * small split batches) run "cn_sub_kernel" instead (16-frame sub-tiles, t in
+ * registers, 16 B/edge); the LDPC_K_CN profile kind counts whichever ran. */
 const char *ldpc_cn_kernel_name(const ldpc_graph *g);
 /* LDS bytes per workgroup of the tile-resident decoder for this graph, or 0 if
  * it does not apply.  It needs H_std = [A | I_m] and the A column sums of the
@@ -214,7 +217,7 @@ int ldpc_phys_mc_run(ldpc_decoder *d_std, const ldpc_graph *g_phys, uint64_t see
  * synchronises, returns the summed milliseconds and launch counts per kind
  * (LDPC_K_*), and resets the accumulators.
  */
-#define LDPC_K_CN 0      /* cn_kernel / cn_row_kernel (+ cn_rare_kernel): the split path's CN */
+#define LDPC_K_CN 0      /* cn_kernel / cn_row_kernel / cn_sub_kernel (+ cn_rare_kernel): the split path's CN */
 #define LDPC_K_VN 1      /* vn_kernel: the split path's per-tile VN */
 #define LDPC_K_GEN 2
 #define LDPC_K_COUNT 3

@@ -39,8 +39,8 @@ __device__ __forceinline__ bool div_nr_ok(double P) {
     return __ballot(!(__builtin_fabs(P) >= kDivNrMin)) == 0ull;
 }
 
-// ---- math tables in LDS: 9 x 16 tanh pairs + the atanh table (216 pairs:
-// 5.6 KB; the log form, LDPC_ATANH_TAB=0: 128 log entries, 6.4 KB)
+// ---- math tables in LDS: 9 x 16 tanh pairs + atanh_f's log table (128
+// entries padded to 32 B: 4 KB)
 struct LdsTanh {
     const Pair *p;
     __device__ __forceinline__ Pair operator()(int pp, int i) const { return p[pp * 16 + i]; }
@@ -48,27 +48,16 @@ struct LdsTanh {
 struct alignas(16) LogEntry4 {
     double invc, hi, lo, pad;
 };
-#if LDPC_ATANH_TAB
-using AtanhEntry = Pair;
-constexpr int kAtanhEntries = kAtabN;
-#else
-using AtanhEntry = LogEntry4;
-constexpr int kAtanhEntries = 128;
-#endif
 struct LdsAtanh {
-    const AtanhEntry *e;
-#if LDPC_ATANH_TAB
-    __device__ __forceinline__ Pair operator()(int i) const { return e[i]; }
-#else
+    const LogEntry4 *e;
     __device__ __forceinline__ LogEntry operator()(int i) const {
         const LogEntry4 v = e[i];
         return {v.invc, v.hi, v.lo};
     }
-#endif
 };
 struct MathLds {
     Pair tanh[9 * 16];
-    AtanhEntry atanh[kAtanhEntries];
+    LogEntry4 atanh[128];
 };
 
 __device__ __forceinline__ void fill_math_lds(MathLds &m) {
@@ -77,12 +66,8 @@ __device__ __forceinline__ void fill_math_lds(MathLds &m) {
         m.tanh[k] = pp == 0 ? Pair{dfrom(tab::kTanhB[i]), dfrom(tab::kTanhC[0][i])}
                             : Pair{dfrom(tab::kTanhC[2 * pp - 1][i]), dfrom(tab::kTanhC[2 * pp][i])};
     }
-#if LDPC_ATANH_TAB
-    for (int i = threadIdx.x; i < kAtabN; i += blockDim.x) m.atanh[i] = {dfrom(tab::kAtab[i][0]), dfrom(tab::kAtab[i][1])};
-#else
     for (int i = threadIdx.x; i < 128; i += blockDim.x)
         m.atanh[i] = {dfrom(tab::kLog[i][0]), dfrom(tab::kLog[i][1]), dfrom(tab::kLog[i][2]), 0.0};
-#endif
 }
 
 // t = tanh(M/2) with the reference's clip (:138-146) applied to the output:

@@ -36,15 +36,6 @@
 namespace ldpc {
 namespace {
 
-#ifndef LDPC_CS_PRE
-#define LDPC_CS_PRE 0
-#endif
-#ifndef LDPC_CS_S20
-#define LDPC_CS_S20 4  // phase-1 load stages of the 8 x 20 shape
-#endif
-#ifndef LDPC_CS_WPS20
-#define LDPC_CS_WPS20 6  // its register cap (min wavefronts per SIMD)
-#endif
 constexpr int kCsQ = 4;   // lane groups per wavefront
 constexpr int kCsF = 16;  // frames per workgroup (lane = group * 16 + frame)
 
@@ -121,14 +112,6 @@ __global__ __launch_bounds__(64 * W, WPS) void cn_sub_kernel(DevGraph g, DevStat
 
     double t[K];
     bool tiny = false;
-    // LDPC_CS_PRE (A/B): every slot's column index is requested up front (one
-    // round trip for the whole row instead of one per stage)
-    int colp[LDPC_CS_PRE ? K : 1];
-    if (LDPC_CS_PRE) {
-#pragma unroll
-        for (int i = 0; i < (LDPC_CS_PRE ? K : 1); ++i)
-            colp[i] = i < CS ? (int)g.col16[min(e0 + i, elast)] : 0;
-    }
 #pragma unroll
     for (int h = 0; h < S; ++h) {
         constexpr int H = K / S;
@@ -138,7 +121,7 @@ __global__ __launch_bounds__(64 * W, WPS) void cn_sub_kernel(DevGraph g, DevStat
 #pragma unroll
             for (int q = 0; q < H; ++q) {
                 const int e = min(e0 + h * H + q, elast);
-                col[q] = LDPC_CS_PRE ? colp[(h * H + q) % (LDPC_CS_PRE ? K : 1)] : col_idx[e];
+                col[q] = col_idx[e];
                 eo[q] = kFirst ? 0.0 : cs_ld_e(&Et[(size_t)e * g.ef]);
             }
 #pragma unroll
@@ -209,20 +192,12 @@ __global__ __launch_bounds__(64 * W, WPS) void cn_sub_kernel(DevGraph g, DevStat
 }  // namespace
 
 // The shapes: rows <= 8*4*20 = 640 edges (wimax_2304_0.5: 416-632) in 8
-// wavefronts x 20 slots; rows <= 8*4*30 = 960 (the r3/4 codes: <= 931) in 8 x 30.
-// LDPC_CS_W16 (A/B): the r3/4 rows in 16 wavefronts x 15 slots instead.
-#ifndef LDPC_CS_W16
-#define LDPC_CS_W16 0
-#endif
-// LDPC_CS_R12 (A/B): the rows of <= 640 edges in 16 wavefronts x 10 slots
-// (<= 64 VGPRs: two 16-wavefront workgroups per CU) instead of 8 x 20.
-#ifndef LDPC_CS_R12
-#define LDPC_CS_R12 0
-#endif
+// wavefronts x 20 slots, phase-1 loads in 4 stages, >= 6 wavefronts per SIMD;
+// rows <= 8*4*30 = 960 (the r3/4 codes: <= 931) in 8 x 30.  Measured and not
+// kept (profiles/r4b_ab, r4c_ab): 16 x 10 and 16 x 15 shapes, indices
+// requested up front, other stage counts.
 int cn_sub_shape(const DevGraph &g) {
-    if (LDPC_CS_R12 && g.max_row_deg <= 16 * kCsQ * 10) return 10;
     if (g.max_row_deg <= 8 * kCsQ * 20) return 20;
-    if (LDPC_CS_W16 && g.max_row_deg <= 16 * kCsQ * 15) return 15;
     if (g.max_row_deg <= 8 * kCsQ * 30) return 30;
     return 0;
 }
@@ -233,22 +208,11 @@ static hipError_t launch_cn_sub_t(const DevGraph &g, const DevState &st, int par
     const int *ci = g.col_idx, *rp = g.row_ptr;
     switch (cn_sub_shape(g)) {
         case 20:
-            cn_sub_kernel<kFirst, kStream, 8, 20, LDPC_CS_S20, LDPC_CS_WPS20><<<grid, 64 * 8, 0, s>>>(g, st, par, ci, rp,
-                                                                                      kAtanhCoef);
+            cn_sub_kernel<kFirst, kStream, 8, 20, 4, 6><<<grid, 64 * 8, 0, s>>>(g, st, par, ci, rp, kAtanhCoef);
             break;
         case 30:
             cn_sub_kernel<kFirst, kStream, 8, 30, 6, 4><<<grid, 64 * 8, 0, s>>>(g, st, par, ci, rp, kAtanhCoef);
             break;
-#if LDPC_CS_R12
-        case 10:
-            cn_sub_kernel<kFirst, kStream, 16, 10, 2, 8><<<grid, 64 * 16, 0, s>>>(g, st, par, ci, rp, kAtanhCoef);
-            break;
-#endif
-#if LDPC_CS_W16
-        case 15:
-            cn_sub_kernel<kFirst, kStream, 16, 15, 3, 4><<<grid, 64 * 16, 0, s>>>(g, st, par, ci, rp, kAtanhCoef);
-            break;
-#endif
         default:
             return hipErrorInvalidValue;
     }

@@ -48,7 +48,6 @@ struct ldpc_graph {
     std::vector<int> h_row_ptr, h_col_idx;
     int *d_ints = nullptr;       // one allocation for all index arrays
     uint32_t *d_apack = nullptr;  // bit-packed A (std_form graphs only)
-    uint16_t *d_col16 = nullptr;  // col_idx as uint16 (n <= 65535)
 };
 
 struct ldpc_decoder {
@@ -497,9 +496,7 @@ int ldpc_graph_create(int32_t m, int32_t n, const int32_t *row_ptr, const int32_
     if (device < 0) (void)hipGetDevice(&g->device);
     const std::vector<int> p3dep = sub_p3_deps(m, row_ptr, col_idx);
     const std::vector<int> p3dep8 = sub_p3_deps(m, row_ptr, col_idx, true);
-    const std::vector<int> p3dep12 = sub_p3_deps<12>(m, row_ptr, col_idx);
-    const size_t nints = (size_t)(m + 1) + nnz + (size_t)(n + 1) + 2 * (size_t)nnz + p3dep.size() + p3dep8.size() +
-                         p3dep12.size();
+    const size_t nints = (size_t)(m + 1) + nnz + (size_t)(n + 1) + 2 * (size_t)nnz + p3dep.size() + p3dep8.size();
     if (int rc = dev_alloc(&g->d_ints, nints)) {
         delete g;
         return rc;
@@ -529,7 +526,6 @@ int ldpc_graph_create(int32_t m, int32_t n, const int32_t *row_ptr, const int32_
     p += p3dep.size();
     G.p3dep8 = p;
     p += p3dep8.size();
-    G.p3dep12 = p;
     hipError_t e = hipSuccess;
     if (e == hipSuccess) e = hipMemcpy((void *)G.row_ptr, row_ptr, sizeof(int) * (m + 1), hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMemcpy((void *)G.col_idx, col_idx, sizeof(int) * nnz, hipMemcpyHostToDevice);
@@ -540,8 +536,6 @@ int ldpc_graph_create(int32_t m, int32_t n, const int32_t *row_ptr, const int32_
         e = hipMemcpy((void *)G.p3dep, p3dep.data(), sizeof(int) * p3dep.size(), hipMemcpyHostToDevice);
     if (e == hipSuccess && m > 0)
         e = hipMemcpy((void *)G.p3dep8, p3dep8.data(), sizeof(int) * p3dep8.size(), hipMemcpyHostToDevice);
-    if (e == hipSuccess && m > 0)
-        e = hipMemcpy((void *)G.p3dep12, p3dep12.data(), sizeof(int) * p3dep12.size(), hipMemcpyHostToDevice);
     if (e == hipSuccess && std_form && k > 0) {  // encoder table: A bit-packed per row
         const size_t kw = (size_t)(k + 31) / 32;
         std::vector<uint32_t> ap((size_t)m * kw, 0u);
@@ -553,20 +547,12 @@ int ldpc_graph_create(int32_t m, int32_t n, const int32_t *row_ptr, const int32_
             e = hipMemcpy(g->d_apack, ap.data(), sizeof(uint32_t) * ap.size(), hipMemcpyHostToDevice);
         G.a_packed = g->d_apack;
     }
-    if (e == hipSuccess && n <= 65535) {
-        std::vector<uint16_t> c16(col_idx, col_idx + nnz);
-        if (dev_alloc(&g->d_col16, c16.size())) e = hipErrorOutOfMemory;
-        if (e == hipSuccess)
-            e = hipMemcpy(g->d_col16, c16.data(), sizeof(uint16_t) * c16.size(), hipMemcpyHostToDevice);
-        G.col16 = g->d_col16;
-    }
     // the WiMAX 2304 codes run the 8-frame sub-tile decoder: E in 8-frame blocks
     if (e == hipSuccess && !ldpc::tile64_lds_bytes(G) && ldpc::tile8_applies(G)) G.ef = 8;
     if (e != hipSuccess) {
         (void)hipFree(g->d_ints);
         (void)hipFree(g->d_apack);
-        (void)hipFree(g->d_col16);
-        delete g;
+            delete g;
         return ldpc_fail(LDPC_EDEVICE, "ldpc_graph_create: upload failed: %s", hipGetErrorString(e));
     }
     *out = g;
@@ -578,7 +564,6 @@ int ldpc_graph_destroy(ldpc_graph *g) {
     DeviceGuard dg(g->device);
     (void)hipFree(g->d_ints);
     (void)hipFree(g->d_apack);
-    (void)hipFree(g->d_col16);
     delete g;
     return LDPC_OK;
 }

@@ -10,7 +10,6 @@ namespace ldpc {
 constexpr float kPhiMin = 1.0e-7f;  // phi(1e-7) ~ 16.8: caps the magnitude
 constexpr float kPhiMax = 30.0f;    // phi(30) ~ 1.9e-13
 
-#ifndef LDPC_PHYS_ACCURATE_PHI
 // phi(x) = log((e^x + 1)/(e^x - 1)) with the hardware v_exp_f32 / v_log_f32 /
 // v_rcp_f32 (one instruction each).  Below x = 2^-5 the quotient loses bits to
 // e^x - 1, so use the series phi(x) ~ log(2/x) + x^2/12 there.
@@ -20,11 +19,5 @@ __device__ __forceinline__ float phi(float x) {
     const float t = __expf(x);
     return __logf((t + 1.0f) * __frcp_rn(t - 1.0f));
 }
-#else
-__device__ __forceinline__ float phi(float x) {
-    x = fminf(fmaxf(x, kPhiMin), kPhiMax);
-    return log1pf(2.0f / expm1f(x));  // -log(tanh(x/2))
-}
-#endif
 
 }  // namespace ldpc

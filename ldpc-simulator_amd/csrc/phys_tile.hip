@@ -33,19 +33,12 @@
 namespace ldpc {
 namespace {
 
-// LDPC_PHYS_NT 1: the fp32 message array (streamed once per pass in each
-// direction, far larger than L2) is loaded / stored non-temporally, so the
-// gathers of L keep L2 to themselves (as the parity kernels' E stream).
-#ifndef LDPC_PHYS_NT
-#define LDPC_PHYS_NT 1
-#endif
-__device__ __forceinline__ float ld_e32(const float *p) { return LDPC_PHYS_NT ? __builtin_nontemporal_load(p) : *p; }
-__device__ __forceinline__ void st_e32(float *p, float v) {
-    if (LDPC_PHYS_NT)
-        __builtin_nontemporal_store(v, p);
-    else
-        *p = v;
-}
+// The fp32 message array (streamed once per pass in each direction, far
+// larger than L2) is loaded / stored non-temporally, so the gathers of L keep
+// L2 to themselves (as the parity kernels' E stream; +2-3 %,
+// profiles/r1u_nt/ab_phys_nt.txt).
+__device__ __forceinline__ float ld_e32(const float *p) { return __builtin_nontemporal_load(p); }
+__device__ __forceinline__ void st_e32(float *p, float v) { __builtin_nontemporal_store(v, p); }
 
 
 constexpr int kRowsPerWave = 4;

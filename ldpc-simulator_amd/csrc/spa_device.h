@@ -42,10 +42,7 @@ struct DevGraph {
     const uint32_t *a_packed;  // [m][kw] bit j of row r = A[r][j] (encoder; std_form only)
     const int *p3dep;          // [m][16] sub-tile S order: lo | hi << 8 (tile_sub.hip sub_p3)
     const int *p3dep8;         // [m][16] the same over each row's A edges (tile8.hip: identity excluded)
-    const int *p3dep12;        // [m][12] p3dep for 12 wavefronts (tile_sub.hip, LDPC_SUB_WAVES=12 A/B)
     int ef;                    // frames per E block (64, or 8 for tile8.hip's graphs): e_base
-    const uint16_t *col16;     // [nnz] col_idx as uint16 (n <= 65535; else null): the tile kernels'
-                               // index staging reads half the bytes (L2 footprint shared with the L gather)
 };
 
 // E layout inside a tile: the 64 frames in blocks of g.ef, each block

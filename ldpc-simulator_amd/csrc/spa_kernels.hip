@@ -50,33 +50,17 @@ namespace {
 
 constexpr int kCnRowsPerBlock = 4;           // 4 wavefronts = 4 rows of one tile
 constexpr int kVnWaves = 16;                 // wavefronts per VN workgroup
-#ifndef LDPC_PV
-#define LDPC_PV 4
-#endif
-constexpr int kPv = LDPC_PV;                 // VN column-sum loads in flight
+constexpr int kPv = 4;                       // VN column-sum loads in flight
 
 // --------------------------------------------------------------- CN pass
-#ifndef LDPC_CN_WAVES
-#define LDPC_CN_WAVES 7  // min wavefronts per SIMD for cn_kernel (register budget)
-#endif
-#ifndef LDPC_PF
-#define LDPC_PF 4
-#endif
-constexpr int kPf = LDPC_PF;  // edges in flight per wavefront (software pipeline depth)
+constexpr int kCnWaves = 7;  // min wavefronts per SIMD for cn_kernel (register budget)
+constexpr int kPf = 4;       // edges in flight per wavefront (software pipeline depth; 6 and 8 measured no faster, profiles/r3_ab/ab_pf)
 
-// LDPC_SPLIT_NT 1: the message array E (streamed once per pass, far larger
-// than L2) is loaded and stored non-temporally by the CN/VN kernels, so it
-// does not evict the tiles' posteriors (the L[col] gather) from L2.
-#ifndef LDPC_SPLIT_NT
-#define LDPC_SPLIT_NT 1
-#endif
-__device__ __forceinline__ double ld_e(const double *p) { return LDPC_SPLIT_NT ? __builtin_nontemporal_load(p) : *p; }
-__device__ __forceinline__ void st_e(double *p, double v) {
-    if (LDPC_SPLIT_NT)
-        __builtin_nontemporal_store(v, p);
-    else
-        *p = v;
-}
+// The message array E (streamed once per pass, far larger than L2) is loaded
+// and stored non-temporally by the CN/VN kernels, so it does not evict the
+// tiles' posteriors (the L[col] gather) from L2 (profiles/r1u_nt).
+__device__ __forceinline__ double ld_e(const double *p) { return __builtin_nontemporal_load(p); }
+__device__ __forceinline__ void st_e(double *p, double v) { __builtin_nontemporal_store(v, p); }
 
 // Register ring of the next kPf edges' (L[col], E_old) loads.  take(k, e)
 // returns M for edge e (ring slot k) and issues the loads for edge e + kPf.
@@ -110,7 +94,7 @@ struct EdgeStream {
     }
 };
 template <bool kFirst, bool kStream>
-__global__ __launch_bounds__(256, LDPC_CN_WAVES) void cn_kernel(DevGraph g, DevState st, int blocks_per_tile,
+__global__ __launch_bounds__(256, kCnWaves) void cn_kernel(DevGraph g, DevState st, int blocks_per_tile,
                                                                 int it_parity, const int *__restrict__ col_idx,
                                                                 const int *__restrict__ row_ptr, AtanhCoef ac) {
     __shared__ MathLds mlds;

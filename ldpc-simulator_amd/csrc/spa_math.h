@@ -10,15 +10,10 @@
 //          coefficients sit in LDS as {b,c0},{c1,c2},...,{c15,c16} pairs:
 //          9 ds_read_b128 + 16 v_fma_f64 per call.
 // atanh_f  atanh for |q| <= CL (spa_decoder.py:167-168), our design:
-//          |q| < 2^-5: odd Taylor polynomial; else (default, LDPC_ATANH_TAB=0)
-//          the log form below.  LDPC_ATANH_TAB=1 (A/B, round 4): the addition
-//          formula atanh(a) = atanh(c) + atanh((a-c)/(1-ac)) at the centre c
-//          of a's table interval (4 per binade of a, or of 1-a above 1/2),
-//          atanh(c) a double-double from a 216-entry table -- one reciprocal
-//          instead of two, 25 % fewer VALU per call, correctly rounded on
-//          99.97 % of inputs, yet no faster in the kernels (latency-bound;
-//          the static headline spills 6 more registers: 0.441 vs 0.453,
-//          3 dB point 86.5k vs 88.0k cw/s, profiles/r4n_ab).
+//          |q| < 2^-5: odd Taylor polynomial; else the log form below.
+//          (A table form, atanh(c) + atanh((a-c)/(1-ac)) at the centre c of
+//          a's interval, had 25 % fewer VALU per call and was no faster in the
+//          kernels -- latency-bound, more spills: profiles/r4n_ab; git history.)
 //          The log form: atanh(a) = log(y)/2 with
 //          y = (1+a)/(1-a) carried as a double-double (faithful quotient +
 //          exact fma residual + the exact rounding errors of 1+a and 1-a), the
@@ -230,53 +225,6 @@ __host__ __device__ __forceinline__ double atanh_small(double q, const AtanhCoef
     return dfrom(dbits(res) | (dbits(q) & 0x8000000000000000ull));
 }
 
-#ifndef LDPC_ATANH_TAB
-#define LDPC_ATANH_TAB 0
-#endif
-constexpr int kAtabN = 216;  // spa_math_tables.h kAtab
-
-// atanh(a) for 2^-5 <= a <= CL (the table form).  Interval: a's binade and
-// top 2 mantissa bits for a <= 1/2 (entries 0..19), else those of v = 1 - a
-// (exact; entries 20..215); centre x_i = 2^e (1 + m/4 + 1/8), c = x_i or
-// 1 - x_i (exact).  d = (a - c)/(1 - a c): the numerator is exact
-// (Sterbenz), the denominator one fma rounding whose error is recovered, the
-// quotient d0 = num * rcp with both corrections carried as dlo; |d| <= 0.088, so atanh(d) - d = d^3 (1/3
-// + d^2/5 + ... + d^12/15) to 2^-56.  atanh(a) = T_hi + (d0 + (T_lo + dlo +
-// d^3 p)), the first sum split exactly (|T_hi| >= |d0|).
-template <class AtabT>
-__host__ __device__ __forceinline__ double atanh_tab_abs(double a, const AtabT &tb, const AtanhCoef &k) {
-    const bool r2 = a > 0.5;
-    const double x = r2 ? 1.0 - a : a;
-    const uint64_t ux = dbits(x);
-    const double xi = dfrom((ux & 0xFFFC000000000000ull) | (1ull << 49));
-    const double c = r2 ? 1.0 - xi : xi;
-    const int ef = (int)(ux >> 52), m2 = (int)(ux >> 50) & 3;
-    const int idx = r2 ? 20 + (ef - 973) * 4 + m2 : (ef - 1018) * 4 + m2;
-    const double num = a - c;
-    const double den = __builtin_fma(-a, c, 1.0);
-    // den's own rounding error: 1 - a c = (1 - den) - x x_i for a <= 1/2
-    // ((1 - den) exact, den >= 0.71), = (x + x_i - den) - x x_i above (x + x_i
-    // exact: both multiples of 2^-53 below 1/2; the difference exact by
-    // Sterbenz), one fma rounding either way
-    const double ed = __builtin_fma(-x, xi, (r2 ? x + xi : 1.0) - den);
-    const double r = fast_rcp(den);
-    const double d0 = num * r;
-    // the quotient's tail: its exact residual, and den's error, over den
-    const double dlo = __builtin_fma(-(d0 * r), ed, __builtin_fma(-d0, den, num) * r);
-    const double d2 = d0 * d0;
-    double p = __builtin_fma(d2, k.t15, k.t13);
-    p = __builtin_fma(p, d2, k.t11);
-    p = __builtin_fma(p, d2, k.t9);
-    p = __builtin_fma(p, d2, k.t7);
-    p = __builtin_fma(p, d2, k.t5);
-    p = __builtin_fma(p, d2, k.t3);
-    const double tail = __builtin_fma(d0 * d2, p, dlo);
-    const Pair t = tb(idx);
-    const double s = t.a + d0;
-    const double err = (t.a - s) + d0;  // exact: |t.a| >= |d0|
-    return s + (err + (t.b + tail));
-}
-
 // atanh(q) for |q| <= CL.
 template <class LogTab>
 __host__ __device__ __forceinline__ double atanh_f(double q, const LogTab &lt, const AtanhCoef &c = kAtanhCoef) {
@@ -284,8 +232,6 @@ __host__ __device__ __forceinline__ double atanh_f(double q, const LogTab &lt, c
     double res;
     if (a < kAtanhSmall) {
         res = atanh_small_abs(a, c);
-    } else if constexpr (LDPC_ATANH_TAB != 0) {
-        res = atanh_tab_abs(a, lt, c);
     } else {
         // atanh(a) = log(y)/2, y = (1+a)/(1-a) carried as y_hi + y_lo:
         // u = 1+a and v = 1-a are rounded, their errors cu, cv exact (u-1, v-1
@@ -318,14 +264,6 @@ struct HostLogTab {
         return {dfrom(tab::kLog[i][0]), dfrom(tab::kLog[i][1]), dfrom(tab::kLog[i][2])};
     }
 };
-// the table atanh_f reads in the compiled form (LDPC_ATANH_TAB)
-struct HostAtabTab {
-    __host__ Pair operator()(int i) const { return {dfrom(tab::kAtab[i][0]), dfrom(tab::kAtab[i][1])}; }
-};
-#if LDPC_ATANH_TAB
-using HostAtanhTab = HostAtabTab;
-#else
-using HostAtanhTab = HostLogTab;
-#endif
+using HostAtanhTab = HostLogTab;  // the table atanh_f reads
 
 }  // namespace ldpc

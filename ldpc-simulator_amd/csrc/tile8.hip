@@ -59,18 +59,6 @@ constexpr int kF8 = 8;          // frames per workgroup
 constexpr int kQ8 = 8;          // lane groups per wavefront
 constexpr int kSR8 = 8;         // chain slots (>= 2 D: a slot is reused only after every P3 of its row)
 constexpr size_t kLds8Max = 163840;
-// Scheduling fences between the slots of P1 (tanh) and P3 (atanh): without
-// them the compiler interleaves all K slots' math for ILP and spills; the
-// four wavefronts of a SIMD supply the overlap instead.
-#ifndef LDPC_T8_SLOT_FENCE
-#define LDPC_T8_SLOT_FENCE 0
-#endif
-__device__ __forceinline__ void t8_slot_fence() {
-#if LDPC_T8_SLOT_FENCE
-    __builtin_amdgcn_sched_barrier(0);
-#endif
-}
-
 // -DLDPC_T8_TIMERS: diagnostic build (never the product) -- s_memtime phase
 // timers per wavefront, printed for two workgroups at the end of the launch.
 #ifdef LDPC_T8_TIMERS
@@ -93,12 +81,7 @@ __device__ __forceinline__ int t8_wave(int hw) { return (hw & 3) * 4 + (hw >> 2)
 // the prefetched E_old).  NT = non-temporal (the message stream).
 typedef unsigned int t8u2 __attribute__((ext_vector_type(2)));
 constexpr int kNT = 2;
-// LDPC_EST_SC1 (A/B): E_new stores sc1 (aux bit 4: written through and dropped
-// from L2) instead of nt, which keeps the line (MI355X_MICROARCH.md)
-#ifndef LDPC_EST_SC1
-#define LDPC_EST_SC1 0
-#endif
-constexpr int kEStAux = LDPC_EST_SC1 ? 16 : kNT;
+constexpr int kEStAux = kNT;  // E_new stores nt (sc1 write-through measured slower: 0.350 vs 0.362, profiles/r4b_ab)
 // a voffset past every buffer's num_records: the hardware drops such a store
 // (and a load returns 0) -- masked stores without a branch
 constexpr uint32_t kOOB = 0xfffffff0u;
@@ -167,7 +150,6 @@ __device__ __forceinline__ T8Chunk t8_chunk(const int *__restrict__ row_ptr, int
 template <int K>
 struct T8Ctx {
     const int *__restrict__ col_idx;
-    const uint16_t *__restrict__ col16;
     const int *__restrict__ row_ptr;
     const int *p3dep;
     // buffer resources (uniform) + per-lane byte offsets eo8 (E block: f * 8)
@@ -221,10 +203,6 @@ __device__ __forceinline__ int t8_stage_issue(const T8Ctx<K> &c, int q) {
     if (q >= c.m) return 0;
     const T8Chunk rc = t8_chunk(c.row_ptr, q, c.wave);
     const int L = threadIdx.x & 63;
-#ifndef LDPC_COL16
-#define LDPC_COL16 0
-#endif
-    if (LDPC_COL16) return rc.cnt > 0 ? (int)c.col16[rc.c0 + min(L, rc.cnt - 1)] : 0;
     return rc.cnt > 0 ? c.col_idx[rc.c0 + min(L, rc.cnt - 1)] : 0;
 }
 template <int K>
@@ -248,130 +226,69 @@ struct T8Pre {
     double eo[K];
     double lid, eid;  // wavefront 0: the identity column's posterior and E_old
 };
-// Slots [I0, I1) of the E_old loads (the L-gathering variant may issue its
-// first LDPC_T8_PF slots one body early, the rest at P1: a register budget A/B).
-#ifndef LDPC_T8_PF
-#define LDPC_T8_PF 0
-#endif
-// LDPC_FRESH_NOLOAD: a fresh streaming frame's lanes skip the E_old loads
-// (exec-masked; M = L for them), as tile_sub.hip
-#ifndef LDPC_FRESH_NOLOAD
-#define LDPC_FRESH_NOLOAD 1
-#endif
-template <int K, int I0 = 0, int I1 = K, bool kId = true>
+// (iteration 0 and a fresh streaming frame's lanes form M = L - 0.0 == L and
+// read no E_old: exec-masked)
+template <int K>
 __device__ __forceinline__ void t8_prefetch(const T8Ctx<K> &c, int r, T8Pre<K> &p) {
     const T8Chunk rc = t8_chunk(c.row_ptr, r, c.wave);
-    if (rc.cnt > 0) {  // iteration 0 forms M = L - 0.0 (== L exactly) and reads no E_old
+    if (rc.cnt > 0) {
         const uint32_t eoff = t8_eoff(c, rc);
 #pragma unroll
-        for (int i = I0; i < I1; ++i)
-            p.eo[i] = (c.first || (LDPC_FRESH_NOLOAD && c.fresh)) ? 0.0 : t8_ld<kNT>(c.rE, t8_es(c, eoff, i));
+        for (int i = 0; i < K; ++i) p.eo[i] = (c.first || c.fresh) ? 0.0 : t8_ld<kNT>(c.rE, t8_es(c, eoff, i));
     }
-    if (kId && c.wave == c.idwave && rc.deg > 0) {  // identity edge (a fresh streaming frame has L = ch: gen_slots)
+    if (c.wave == c.idwave && rc.deg > 0) {  // identity edge (a fresh streaming frame has L = ch: gen_slots)
         p.lid = t8_ld(c.first ? c.rC : c.rL, ((uint32_t)(c.k + r) << 9) + c.lo8);
-        p.eid = (c.first || (LDPC_FRESH_NOLOAD && c.fresh)) ? 0.0 : t8_ld<kNT>(c.rE, ((uint32_t)(rc.beg + rc.deg - 1) << 6) + c.eo8);
+        p.eid = (c.first || c.fresh) ? 0.0 : t8_ld<kNT>(c.rE, ((uint32_t)(rc.beg + rc.deg - 1) << 6) + c.eo8);
     }
 }
 
 // P1: t = tanh((L[col] - E_old)/2) for this lane's slots, columns into col[];
 // returns whether some lane's own edge has |t| <= 1e-10 (:159).  Every slot is
-// evaluated (branch-free): slots past the piece hold valid data and end as 1.0.
-// LDPC_T8_KDISP (A/B): P1 and the hop run only the slots the row's pieces can
-// use -- KK = K - 1 when the row's piece length CS < K (wave-uniform; 561 of the
-// 576 rows of wimax_2304_0.75A have CS = 7 of K = 8), K otherwise -- instead of
-// all K (the padded slots cost a tanh and a chain multiply each).
-#ifndef LDPC_T8_KDISP
-#define LDPC_T8_KDISP 2
-#endif
-// LDPC_T8_LDSADD: P3's column-sum updates as ds_add_f64 (as tile_sub.hip's
-// LDPC_SUB_LDSADD: the same IEEE adds in the same order, no read round trip)
-#ifndef LDPC_T8_LDSADD
-#define LDPC_T8_LDSADD 1
-#endif
-// LDPC_T8_SATMEMO: P3 reuses slot 0's E_new for the slots whose quotients all
-// have slot 0's magnitude (t8_p3; saturated rows: config 4's 3.5 / 4 dB points,
-// +23 % there, -0.7 % at 1 dB, profiles/r4w_ab)
-#ifndef LDPC_T8_SATMEMO
-#define LDPC_T8_SATMEMO 1
-#endif
-// The P1 half (LDPC_T8_SATP1=1, A/B, not the default): a pass flagged
-// saturated by t8_sat_next runs a P1 form that gives a slot t = +-CL without
-// the tanh polynomial where every lane's |M| >= 35.  profiles/r4w_ab: +9 % at
-// 3.5 dB alone, but -4.5 % at 1 dB (the second row-loop copy doubles the
-// kernel's code) and less than the P3 half with it (7,026 vs 6,838 cw/s)
-#ifndef LDPC_T8_SATP1
-#define LDPC_T8_SATP1 0
-#endif
-#ifndef LDPC_T8_SATP3  // A/B: the P3 half alone
-#define LDPC_T8_SATP3 LDPC_T8_SATMEMO
-#endif
-template <int K, int KK, bool LA, bool SAT>
+// evaluated (branch-free): slots past the piece hold valid data and end as 1.0
+// -- except slot K-1 of a row whose pieces are shorter than K (wave-uniform;
+// 561 of the 576 rows of wimax_2304_0.75A have CS = 7 of K = 8), which takes
+// 1.0 without its tanh (+3 %, profiles/r4b_ab).  P3 adds each slot's E_new
+// into its column sum with one ds_add_f64 (tile_sub.hip: the same IEEE add,
+// no read round trip) and, on saturated rows, reuses slot 0's E_new (t8_p3).
+template <int K, bool LA>
 __device__ __forceinline__ void t8_p1_slots(const T8Ctx<K> &c, int r, const T8Chunk &rc, const T8Pre<K> &pre,
-                                            double (&t)[K], bool &tiny, bool skip_last = false) {
+                                            double (&t)[K], bool &tiny, bool skip_last) {
     const int nj = t8_nj(c, rc);
     const int njt = c.live ? nj : 0;  // the |t| <= 1e-10 vote: frame-less lanes abstain
     const uint16_t *lc = t8_lcols(c, r, rc);
-    double Lv[KK];
-    int col[KK];
+    double Lv[K];
+    int col[K];
 #pragma unroll
-    for (int i = 0; i < KK; ++i) col[i] = lc[i];
+    for (int i = 0; i < K; ++i) col[i] = lc[i];
     if constexpr (LA) {
 #pragma unroll
-        for (int i = 0; i < KK; ++i) Lv[i] = c.LA[(size_t)col[i] * kF8];
+        for (int i = 0; i < K; ++i) Lv[i] = c.LA[(size_t)col[i] * kF8];
     } else {
         const __amdgpu_buffer_rsrc_t rs = c.first ? c.rC : c.rL;  // iteration 0: M = ch (:85-90)
 #pragma unroll
-        for (int i = 0; i < KK; ++i) Lv[i] = t8_ld(rs, ((uint32_t)col[i] << 9) + c.lo8);
-    }
-    // Slots saturated in every lane that matters (|M| >= 35: d = M/2 is
-    // clipped to +-17.5, t = +-np.tanh(17.5) = +-CL, tests/test_math.py) need
-    // no tanh polynomial -- config 4's 3.5 / 4 dB points, where 99.8 % of the
-    // edges saturate.  Only passes flagged saturated (t8_sat_next) run this
-    // form: its per-slot branches cost the other passes their cross-slot overlap.
-    if constexpr (!SAT) {
-#pragma unroll
-        for (int i = 0; i < KK; ++i) {
-            if (i == KK - 1 && skip_last) {  // wave-uniform: no piece reaches slot K-1 in this row
-                t[i] = 1.0;
-                continue;
-            }
-            // :85-90 / :260-268 (eo = 0.0 on iteration 0; a fresh streaming frame M = L)
-            const double M = c.fresh ? Lv[i] : Lv[i] - pre.eo[i];
-            const double tv = tanh_half_clipped(M, c.ttab);  // :138-146 (spa_math.h)
-            tiny |= i < njt && !(fabs(tv) > kTiny);
-            t[i] = i < nj ? tv : 1.0;  // past the piece: an exact no-op in the product
-            t8_slot_fence();
-        }
-    } else {
-#pragma unroll
-        for (int i = 0; i < KK; ++i) {
-            if (i == KK - 1 && skip_last) {
-                t[i] = 1.0;
-                continue;
-            }
-            const double M = c.fresh ? Lv[i] : Lv[i] - pre.eo[i];
-            const double tv = __ballot(i < njt && !(fabs(M) >= 35.0)) == 0ull
-                                  ? dfrom(dbits(kCL) | (dbits(M) & 0x8000000000000000ull))
-                                  : tanh_half_clipped(M, c.ttab);
-            tiny |= i < njt && !(fabs(tv) > kTiny);
-            t[i] = i < nj ? tv : 1.0;
-            t8_slot_fence();
-        }
+        for (int i = 0; i < K; ++i) Lv[i] = t8_ld(rs, ((uint32_t)col[i] << 9) + c.lo8);
     }
 #pragma unroll
-    for (int i = KK; i < K; ++i) t[i] = 1.0;
+    for (int i = 0; i < K; ++i) {
+        if (i == K - 1 && skip_last) {  // wave-uniform: no piece reaches slot K-1 in this row
+            t[i] = 1.0;
+            continue;
+        }
+        // :85-90 / :260-268 (eo = 0.0 on iteration 0; a fresh streaming frame M = L)
+        const double M = c.fresh ? Lv[i] : Lv[i] - pre.eo[i];
+        const double tv = tanh_half_clipped(M, c.ttab);  // :138-146 (spa_math.h)
+        tiny |= i < njt && !(fabs(tv) > kTiny);
+        t[i] = i < nj ? tv : 1.0;  // past the piece: an exact no-op in the product
+    }
 }
 
-template <int K, bool LA, bool SAT>
+template <int K, bool LA>
 __device__ __forceinline__ bool t8_p1(const T8Ctx<K> &c, int r, const T8Pre<K> &pre, double (&t)[K]) {
     bool tiny = false;
     const int sv = t8_stage_issue(c, r + 1);
     const T8Chunk rc = t8_chunk(c.row_ptr, r, c.wave);
     if (rc.cnt > 0) {
-        if (LDPC_T8_KDISP == 1 && K > 1 && rc.CS < K)
-            t8_p1_slots<K, (K > 1 ? K - 1 : K), LA, SAT>(c, r, rc, pre, t, tiny);
-        else
-            t8_p1_slots<K, K, LA, SAT>(c, r, rc, pre, t, tiny, LDPC_T8_KDISP == 2 && rc.CS < K);
+        t8_p1_slots<K, LA>(c, r, rc, pre, t, tiny, rc.CS < K);
     } else {
 #pragma unroll
         for (int i = 0; i < K; ++i) t[i] = 1.0;
@@ -430,7 +347,7 @@ __device__ __forceinline__ void t8_hop(T8Ctx<K> &c, int r, const double (&t)[K],
         // branch-free: every lane group multiplies all K slots (slots past its
         // piece, and every slot of a group past the chunk, hold 1.0: exact
         // no-ops), so the product ends in group 7 whatever the chunk's length
-        if (LDPC_T8_KDISP != 0 && K > 1 && rc.CS < K) {  // slot K-1 holds 1.0 in every group: skip it
+        if (K > 1 && rc.CS < K) {  // slot K-1 holds 1.0 in every group: skip it
 #pragma unroll
             for (int jj = 0; jj < kQ8; ++jj) {
 #pragma unroll
@@ -502,7 +419,7 @@ __device__ __forceinline__ void t8_p3(T8Ctx<K> &c, int r, double (&t)[K]) {
         };
         if (div_nr_ok(c.live ? P : 1.0)) {  // the IEEE quotient without its scaling steps (cn_common.h)
             if (rc.cnt > 0) {
-                if (LDPC_T8_SATP3 && K == 8) {  // the r3/4 form (the L_A form spills with it)
+                if (K == 8) {  // the r3/4 form (the L_A form spills with it)
                     // Saturated rows (config 4's 3.5 and 4 dB points: 99.8 % of
                     // the edges have |M| >= 35, t = +-CL) give most slots one
                     // quotient magnitude.  atanh_f(clip_cl(q)) is odd in q and
@@ -526,14 +443,12 @@ __device__ __forceinline__ void t8_p3(T8Ctx<K> &c, int r, double (&t)[K]) {
                             else
                                 t[i] = 2.0 * atanh_f(clip_cl(q), c.ltab, c.ac);
                         }
-                        t8_slot_fence();
-                    }
+                                }
                 } else {
 #pragma unroll
                     for (int i = 0; i < K; ++i) {
                         if (i < rc.CS) t[i] = en(div_nr(P, t[i]));
-                        t8_slot_fence();
-                    }
+                                }
                 }
             }
             if (idw) EI = en(div_nr(P, tI));
@@ -607,20 +522,11 @@ __device__ __forceinline__ void t8_p3(T8Ctx<K> &c, int r, double (&t)[K]) {
         // S_col += E_new, rows ascending; a lane's slots never share a column
         // within a row, so all reads, all adds, all writes (one LDS round trip)
         double *sp[K];
-        double sv[K];
 #pragma unroll
         for (int i = 0; i < K; ++i) sp[i] = i < nj ? c.S + (size_t)col[i] * kF8 : c.dummy;
-        if (LDPC_T8_LDSADD) {  // one ds_add_f64 per slot (tile_sub.hip LDPC_SUB_LDSADD); past the piece: `dummy`
 #pragma unroll
-            for (int i = 0; i < K; ++i) __hip_atomic_fetch_add(sp[i], t[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        } else {
-#pragma unroll
-            for (int i = 0; i < K; ++i) sv[i] = *sp[i];
-#pragma unroll
-            for (int i = 0; i < K; ++i) sv[i] = sv[i] + t[i];
-#pragma unroll
-            for (int i = 0; i < K; ++i) *sp[i] = sv[i];
-        }
+        for (int i = 0; i < K; ++i)  // one ds_add_f64 per slot; past the piece: `dummy`
+            __hip_atomic_fetch_add(sp[i], t[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
     if (idw && c.j == 0) {  // identity column: L = ch + (0 + E) (:173-185)
         const double Lj = chI + (0.0 + EI);
@@ -637,26 +543,25 @@ __device__ __forceinline__ void t8_p3(T8Ctx<K> &c, int r, double (&t)[K]) {
 // LA variants prefetch the next row's E_old (and identity loads) before
 // hop + P3; the L-gathering variant (8 slots per lane) has no registers for
 // that and issues them at the start of P1.
-template <int K, bool LA, int D, int B, bool SAT>
+template <int K, bool LA, int D, int B>
 __device__ __forceinline__ void t8_body(T8Ctx<K> &c, int r, double (&t)[D][K], bool (&y)[D]) {
     constexpr int N = (B + 1) % D;
     T8Pre<K> pre;
     T8_STAMP(a0);
     if (LA && r + 1 < c.m) t8_prefetch(c, r + 1, pre);
-    if (!LA && LDPC_T8_PF > 0 && r + 1 < c.m) t8_prefetch<K, 0, (LDPC_T8_PF < K ? LDPC_T8_PF : K), false>(c, r + 1, pre);
     T8_STAMP(a1);
     T8_ADD(c, 7, a0, a1);
     if (r < c.m) t8_hop(c, r, t[B], y[B]);
     if (r >= D - 1) t8_p3(c, r - (D - 1), t[N]);
     T8_STAMP(a2);
-    if (!LA && r + 1 < c.m) t8_prefetch<K, (LDPC_T8_PF < K ? LDPC_T8_PF : K), K, true>(c, r + 1, pre);
-    if (r + 1 < c.m) y[N] = t8_p1<K, LA, SAT>(c, r + 1, pre, t[N]);
+    if (!LA && r + 1 < c.m) t8_prefetch(c, r + 1, pre);
+    if (r + 1 < c.m) y[N] = t8_p1<K, LA>(c, r + 1, pre, t[N]);
     T8_STAMP(a3);
     T8_ADD(c, 6, a2, a3);
 }
 
 // One pass over all rows (every P3 done on return, before the barrier).
-template <int K, bool LA, int D, bool SAT>
+template <int K, bool LA, int D>
 __device__ __forceinline__ void t8_rows(T8Ctx<K> &c) {
     const int m = c.m;
     double t[D][K];
@@ -666,14 +571,14 @@ __device__ __forceinline__ void t8_rows(T8Ctx<K> &c) {
         t8_stage_commit(c, 0, t8_stage_issue(c, 0));
         T8Pre<K> pre;
         t8_prefetch(c, 0, pre);
-        y[0] = t8_p1<K, LA, SAT>(c, 0, pre, t[0]);
+        y[0] = t8_p1<K, LA>(c, 0, pre, t[0]);
     }
     const int last = m + D - 2;  // body(last) runs P3(m-1)
     for (int r = 0; r <= last; r += D) {
-        t8_body<K, LA, D, 0, SAT>(c, r, t, y);
-        if (r + 1 <= last) t8_body<K, LA, D, 1, SAT>(c, r + 1, t, y);
+        t8_body<K, LA, D, 0>(c, r, t, y);
+        if (r + 1 <= last) t8_body<K, LA, D, 1>(c, r + 1, t, y);
         if constexpr (D == 3)
-            if (r + 2 <= last) t8_body<K, LA, D, 2, SAT>(c, r + 2, t, y);
+            if (r + 2 <= last) t8_body<K, LA, D, 2>(c, r + 2, t, y);
     }
 }
 
@@ -685,7 +590,6 @@ __device__ __forceinline__ void t8_setup(T8Ctx<K> &c, unsigned char *lds, const 
     int *flags = (int *)(lds + ly.flags);
     const int lane = threadIdx.x & 63;
     c.col_idx = col_idx;
-    c.col16 = g.col16;
     c.row_ptr = row_ptr;
     c.p3dep = g.p3dep8;
     c.wave = uniform(t8_wave(threadIdx.x >> 6));
@@ -733,13 +637,12 @@ __device__ __forceinline__ int t8_epoch0(int pass, int m) {
 template <bool LA>
 __device__ __forceinline__ void t8_vn(const DevGraph &g, double *S, double *LAl, uint32_t *zb, int *cntl,
                                       const int *livel, __amdgpu_buffer_rsrc_t rL, __amdgpu_buffer_rsrc_t rC,
-                                      int sub, bool first, bool fresh_any, const int *freshl, int nllr,
-                                      int *satc) {
+                                      int sub, bool first, bool fresh_any, const int *freshl, int nllr) {
     const int ff = threadIdx.x & 7;
     const uint32_t lo8 = (uint32_t)(sub * kF8 + ff) * 8u;
     const bool live = livel[ff] != 0;
     const bool fr = fresh_any && freshl[ff] != 0;
-    int my_cnt = 0, my_sat = 0;
+    int my_cnt = 0;
     for (int e = threadIdx.x; e < g.k * kF8; e += blockDim.x) {
         const int col = e >> 3;
         const double Sj = S[e];
@@ -757,17 +660,10 @@ __device__ __forceinline__ void t8_vn(const DevGraph &g, double *S, double *LAl,
             my_cnt += (fabs(Lj) <= 7.0 && ap * Lj < 0.0) ? 1 : 0;
         }
         if (LA) LAl[e] = Lj;
-        my_sat += live && fabs(Lj) >= 35.0 ? 1 : 0;
         if (live) t8_st(rL, ((uint32_t)col << 9) + lo8, Lj);
         if (!(Lj < 0.0)) atomicOr(zb + (col >> 5) * kF8 + ff, 1u << (col & 31));
     }
     if (nllr && my_cnt) atomicAdd(cntl + ff, my_cnt);
-    if (LDPC_T8_SATP1 && my_sat) atomicAdd(satc, my_sat);
-}
-// The next pass tests P1's slots for saturation when >= 95 % of the 8 frames'
-// A posteriors have |L| >= 35 (a heuristic: both P1 forms are exact)
-__device__ __forceinline__ bool t8_sat_next(const DevGraph &g, const int *satc) {
-    return LDPC_T8_SATP1 && (long long)*satc * 20 >= (long long)g.k * kF8 * 19;
 }
 
 // syndrome (:191-204): parity of row r = popcount(A_r & (z^1)_A) + (z^1)_{k+r}
@@ -835,28 +731,20 @@ __global__ __launch_bounds__(64 * kW8, 1) void tile8_kernel(DevGraph g, DevState
     c.idwave = D >= 3 ? 0 : kW8 - 1;
     const int fr = tile * kTile + sub * kF8 + c.f;  // this lane's frame
 
-    __shared__ int satc;  // saturated A posteriors of the last pass (t8_vn)
-    if (threadIdx.x == 0) satc = 0;
-    bool satn = false;
     for (int it = 0; it < max_iter; ++it) {
         c.first = it == 0;
         c.live = livel[c.f] != 0;
         c.ep0 = t8_epoch0(it, g.m);
         T8_STAMP(w0);
-        if (!LA && LDPC_T8_SATP1 && satn)  // wave-uniform (LDS count): one form per pass
-            t8_rows<K, LA, D, true>(c);
-        else
-            t8_rows<K, LA, D, false>(c);
+        t8_rows<K, LA, D>(c);
         T8_STAMP(w1);
         T8_ADD(c, 8, w0, w1);
         __syncthreads();  // every P3 done: S complete, identity bits set
         if (threadIdx.x < kW8) c.p3row[threadIdx.x] = 0;
-        t8_vn<LA>(g, S, LAl, zb, cntl, livel, rL, rC, sub, c.first, false, nullptr, nllr, &satc);
+        t8_vn<LA>(g, S, LAl, zb, cntl, livel, rL, rC, sub, c.first, false, nullptr, nllr);
         __syncthreads();
-        satn = t8_sat_next(g, &satc);
         t8_syndrome(g, zb, ib, bad);
         __syncthreads();
-        if (threadIdx.x == 0) satc = 0;  // read by every thread before the barrier above
         if ((threadIdx.x >> 6) == 0) {  // per-frame exits, as vn_kernel (static schedule)
             bool still = false;
             if (lane < kF8 && livel[lane] != 0) {
@@ -924,7 +812,6 @@ __global__ __launch_bounds__(64 * kW8, 1) void tile8_stream_kernel(
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     __shared__ long long gidx[kF8];  // refill: slot f's new frame index (< 0: none)
     __shared__ int nref;             // refill: some slot took a frame this pass
-    __shared__ int satc;             // saturated A posteriors of the last pass (t8_vn)
     const T8Layout ly = t8_layout(g.k, g.m, K, LA, D + 1);
     double *S = (double *)(lds + ly.S);
     double *LAl = LA ? (double *)(lds + ly.LA) : nullptr;
@@ -960,8 +847,6 @@ __global__ __launch_bounds__(64 * kW8, 1) void tile8_stream_kernel(
     const int m = g.m;
     const uint32_t *Ut = st.ubits + (size_t)tile * kw * kTile + sub * kF8 + lane;  // slot lanes only
 
-    if (threadIdx.x == 0) satc = 0;  // ordered before t8_vn's adds by the pass's barriers
-    bool satn = false;
     for (int pass = 0;; ++pass) {
         __syncthreads();  // the previous pass's exits (or the set-up) are visible
         if (w0) {  // refill: slots without a frame take the next indices
@@ -1022,18 +907,13 @@ __global__ __launch_bounds__(64 * kW8, 1) void tile8_stream_kernel(
         c.fresh = freshl[c.f] != 0;
         c.first = false;
         c.ep0 = t8_epoch0(pass, m);
-        if (!LA && LDPC_T8_SATP1 && satn)  // wave-uniform (LDS count): one form per pass
-            t8_rows<K, LA, D, true>(c);
-        else
-            t8_rows<K, LA, D, false>(c);
+        t8_rows<K, LA, D>(c);
         __syncthreads();  // every P3 done: S complete, identity bits set
         if (threadIdx.x < kW8) c.p3row[threadIdx.x] = 0;
-        t8_vn<LA>(g, S, LAl, zb, cntl, livel, rL, rC, sub, false, true, freshl, nllr, &satc);
+        t8_vn<LA>(g, S, LAl, zb, cntl, livel, rL, rC, sub, false, true, freshl, nllr);
         __syncthreads();
-        satn = t8_sat_next(g, &satc);
         t8_syndrome(g, zb, ib, bad);
         __syncthreads();
-        if (threadIdx.x == 0) satc = 0;
         if (w0) {  // per-slot exits and counters (vn_kernel's stream variant)
             unsigned long long cv[7] = {0, 0, 0, 0, 0, 0, 0};
             bool fin = false;

@@ -59,12 +59,6 @@
 #include "spa_math.h"
 #include "frame_source.h"
 
-// LDPC_TILE_LDSADD: tile_kernel's column-sum updates as ds_add_f64 (see
-// tile_sub.hip LDPC_SUB_LDSADD)
-#ifndef LDPC_TILE_LDSADD
-#define LDPC_TILE_LDSADD 1
-#endif
-
 namespace ldpc {
 namespace {
 
@@ -284,10 +278,8 @@ __device__ __forceinline__ void tile_p3(TileCtx &c, int r, double (&t)[kTK]) {
             const int col = c.col_idx[rc.c0 + i];
             if (col < c.k) {  // S_col += E (rows ascending)
                 double *sp = c.S + col * kTile + c.lane;
-                if (LDPC_TILE_LDSADD)  // one ds_add_f64 (tile_sub.hip LDPC_SUB_LDSADD: the same IEEE add)
-                    __hip_atomic_fetch_add(sp, t[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                else
-                    *sp = *sp + t[i];
+                // one ds_add_f64: the same IEEE add as read / add / write (tile_sub.hip)
+                __hip_atomic_fetch_add(sp, t[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             } else {  // identity column: L = ch + (0 + E)  (:173-185)
                 const double Lj = *at(c.Cb, col, c.lane) + (0.0 + t[i]);
                 if (c.live) *at(c.Lb, col, c.lane) = Lj;

@@ -51,22 +51,15 @@
 namespace ldpc {
 namespace {
 
-// wavefronts per workgroup: kSubWaves (16, spa_device.h); LDPC_SUB_WAVES=12
-// (A/B): 3 wavefronts per SIMD with 168 registers each, K = 14 slots per lane
-// (the P3 order table DevGraph::p3dep12): 18 instead of 28 spilled VGPRs, but
-// 0.426 vs 0.452 of HBM at 1 dB (profiles/r4z_ab) -- the fourth wavefront per
-// SIMD hides more latency than the spills cost
-#ifndef LDPC_SUB_WAVES
-#define LDPC_SUB_WAVES 16
-#endif
-constexpr int kSW = LDPC_SUB_WAVES;
-static_assert(kSW == kSubWaves || kSW == 12, "P3 order tables exist for 16 and 12 wavefronts (16 x 64 = the workgroup limit)");
+// wavefronts per workgroup: kSubWaves (16, spa_device.h; 12 wavefronts with
+// 168 registers each spilled less but measured 6 % slower, profiles/r4z_ab)
+constexpr int kSW = kSubWaves;
 constexpr size_t kSubLdsMax = 163840;
 
 template <int Q>
 struct SubCfg {
     static constexpr int F = kTile / Q;           // frames per workgroup
-    static constexpr int K = Q == 4 ? (kSW == 12 ? 14 : 10) : 8;  // slots per lane: row degree <= kSW * Q * K
+    static constexpr int K = Q == 4 ? 10 : 8;  // slots per lane: row degree <= kSW * Q * K
 };
 
 // The product crosses lane groups by v_permlane16/32_swap (Q = 4) or
@@ -77,66 +70,22 @@ struct SubCfg {
 // P3(r-1); the S additions of a row wait on the per-row P3 completion counts,
 // and the chain slots are reused every 4 rows.
 constexpr int kSR = 4;  // chain slots
-// P1: slots per lockstep tanh group (np_tanh_n).  1 is fastest: groups of 2
-// and 3 overlap their table reads but spill (+8 % / 4x time), and the
-// straight-line form of a single slot alone measured 2 % faster than np_tanh
-// behind a per-slot branch (profiles r2u/r2v logs).
-constexpr int kSG = 1;
 // P1 loads and evaluates tanh for all K slots of a lane, branch-free: slots
 // past the chunk's CS hold clamped, valid data (their t ends as 1.0 and is never
 // used), and the straight-line code lets each slot's math wait only for its own
-// loads (+2.7 % over a per-slot branch, profiles r2x logs; the same for P3's
-// E_new math measured neutral).  P3's column-sum additions run as all reads,
-// all adds, all writes: one LDS round trip per row instead of one per slot (a
-// lane's slots never share a column within a row; +1.1 %, profiles r2z logs).
-// Template flag BF selects these forms per kernel: bit 0 the branch-free P1,
-// bit 1 the branch-free P3 (clamped column reads, batched S updates).  The
-// streaming kernel (more live refill state, more spills) took bit 0 only in
-// round 2 (profiles/r2ag_stream_bf); since the round-3 math trims both bits
-// are its best valid form: 2 dB 6.88k (bit 0) vs 7.10k cw/s (both)
-// (profiles/r3_ab/ab_sbf; forms without bit 0 leave the padded slots unset
-// for the branch-free hop: wrong products, caught by
-// tests/test_gpu_config3.py's stream == static check).
-#ifndef SUB_STATIC_BF
-#define SUB_STATIC_BF 3
-#endif
-constexpr int kStaticBF = SUB_STATIC_BF;
-#ifndef SUB_STREAM_BF
-#define SUB_STREAM_BF 3
-#endif
-constexpr int kStreamBF = SUB_STREAM_BF;
-// LDPC_FRESH_NOLOAD (A/B, tile_sub + tile8): iteration 0 / a fresh streaming
-// frame's lanes skip the E_old loads (exec-masked) instead of loading and
-// discarding them (M = L - 0.0 == L either way).
-#ifndef LDPC_FRESH_NOLOAD
-#define LDPC_FRESH_NOLOAD 1
-#endif
-// LDPC_SUB_KDISP (A/B): rows whose pieces are shorter than K (590 of 1152 rows
-// of wimax_2304_0.5 have CS = 9 of K = 10) skip the last slot's tanh and its
-// chain multiplies (one wave-uniform branch per row) instead of padding it.
-#ifndef LDPC_SUB_KDISP
-#define LDPC_SUB_KDISP 0
-#endif
-// LDPC_SUB_LDSADD: P3's column-sum updates as ds_add_f64 instead of read /
-// add / write (one LDS op per slot, no read round trip; +2 % at 1 dB,
-// profiles/r4za_ab).  The same IEEE add of the same operands in the same order
-// (the p3dep waits order a column's additions): ds_add_f64 rounds to nearest
-// even and, unlike the other LDS float atomics, never flushes denormals
-// (LLVM SIISelLowering emits it for workgroup-scope fadd only on that basis)
-#ifndef LDPC_SUB_LDSADD
-#define LDPC_SUB_LDSADD 1
-#endif
-// Timing experiments only (WRONG values by construction, never in a shipped
-// build): LDPC_EXP_NOEOLD drops every E_old load (M = L), LDPC_EXP_NOEST drops
-// every E_new store -- what the message stream costs (profiles/r4o_msg).
-#ifndef LDPC_EXP_NOEOLD
-#define LDPC_EXP_NOEOLD 0
-#endif
-#ifndef LDPC_EXP_NOEST
-#define LDPC_EXP_NOEST 0
-#endif
-// the branch-free hop (Q = 4) multiplies all K slots: P1 must pad them (bit 0)
-static_assert(((kStaticBF & kStreamBF) & 1) != 0, "the branch-free hop needs the branch-free P1");
+// loads (+2.7 % over a per-slot branch, profiles r2x logs); the hop multiplies
+// all K slots of every lane group (the padded 1.0s are exact no-ops).  P3
+// reads clamped column indices for every slot and adds each slot's E_new into
+// its column sum with one ds_add_f64 (slots past the piece add into `dummy`):
+// the same IEEE add of the same operands as read / add / write, rows ordered
+// by the p3dep waits; ds_add_f64 rounds to nearest even and, unlike the other
+// LDS float atomics, never flushes denormals (LLVM SIISelLowering emits it for
+// workgroup-scope fadd only on that basis; +2 %, profiles/r4za_ab).  A fresh
+// streaming frame's lanes (and iteration 0) read no E_old: M = L - 0.0 == L.
+// Measured and not kept (profiles/ READMEs; git history has the code): tanh
+// groups of 2-3 slots in lockstep (spills), guarded per-slot P1/P3 forms,
+// skipping the padded slot K-1 (0.4375), sc1 E_new stores (0.436), uint16
+// index staging (0.417), 12 wavefronts per workgroup (0.426).
 // Logical wavefront (chunk position in a row) of hardware wavefront hw: the
 // four wavefronts of one SIMD (hw = s, s+4, s+8, s+12) take four consecutive
 // chunk positions, so each SIMD holds one contiguous quarter of every row's
@@ -145,18 +94,7 @@ static_assert(((kStaticBF & kStreamBF) & 1) != 0, "the branch-free hop needs the
 // same, spin waits at a lower issue priority +0.2 %).
 __device__ __forceinline__ int sub_wave(int hw) { return (hw & 3) * (kSW / 4) + (hw >> 2); }
 __device__ __forceinline__ double ld_sub_msg(const double *p) { return __builtin_nontemporal_load(p); }
-// LDPC_EST_SC1 (A/B): E_new stored sc1 (the line is written through and
-// dropped from the XCD's L2, MI355X_MICROARCH.md: nt and plain stores keep it,
-// evicting the posteriors the L gather re-reads)
-#ifndef LDPC_EST_SC1
-#define LDPC_EST_SC1 0
-#endif
-__device__ __forceinline__ void st_sub_msg(double *p, double v) {
-    if (LDPC_EST_SC1)
-        __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    else
-        __builtin_nontemporal_store(v, p);
-}
+__device__ __forceinline__ void st_sub_msg(double *p, double v) { __builtin_nontemporal_store(v, p); }
 
 // Column indices of the rows in flight, staged per wavefront in LDS as 16-bit
 // values one row ahead of their P1 (a ring of 3 rows: P3(r-1), P1(r+1) and the
@@ -211,7 +149,6 @@ struct SubCtx {
     static constexpr int F = SubCfg<Q>::F;
     static constexpr int K = SubCfg<Q>::K;
     const int *__restrict__ col_idx;
-    const uint16_t *__restrict__ col16;
     const int *__restrict__ row_ptr;
     // per-lane bases: element (item) of this lane's frame at [item * 64]
     double *Eb;
@@ -263,13 +200,8 @@ template <int Q>
 __device__ __forceinline__ const double *sub_c(const SubCtx<Q> &c, int col) {
     return (const double *)(c.Cu + sub_off(c, col));
 }
-// LDPC_COL16 (A/B): stage the indices from the graph's uint16 copy
-#ifndef LDPC_COL16
-#define LDPC_COL16 0
-#endif
 template <int Q>
 __device__ __forceinline__ int sub_col(const SubCtx<Q> &c, int edge) {
-    if (LDPC_COL16) return *(const uint16_t *)((const char *)c.col16 + ((uint32_t)edge << 1));
     return *(const int *)((const char *)c.col_idx + ((uint32_t)edge << 2));
 }
 // This lane's piece of row r's staged column indices: slot i at [i].  The
@@ -318,7 +250,7 @@ __device__ __forceinline__ void sub_stage_commit(const SubCtx<Q> &c, int q, int 
 // some lane's own edge has |t| <= 1e-10 (:159).  E_old is requested first
 // (independent of the column indices), then the indices, then the posterior
 // gather that needs them.
-template <int Q, int BF>
+template <int Q>
 __device__ __forceinline__ bool sub_p1(const SubCtx<Q> &c, int r, const SubChunk &rc, double (&t)[SubCfg<Q>::K]) {
     constexpr int K = SubCfg<Q>::K;
     bool tiny = false;
@@ -334,53 +266,26 @@ __device__ __forceinline__ bool sub_p1(const SubCtx<Q> &c, int r, const SubChunk
         double eo[K];
 #pragma unroll
         for (int i = 0; i < K; ++i) {
-            if ((BF & 1) || i - i % kSG < rc.CS) {  // guarded form: every slot of a group that runs
-                // a fresh frame's lane reads no E_old (LDPC_FRESH_NOLOAD: on
-                // a streaming pass most slots hold fresh frames)
-                eo[i] = (LDPC_EXP_NOEOLD || (LDPC_FRESH_NOLOAD && c.fresh)) ? 0.0 : ld_sub_msg(sub_es(c, eoff, i));
-                col[i] = lc[i];
-            }
+            // iteration 0 and a fresh frame's lanes read no E_old (on a
+            // streaming pass most slots hold fresh frames)
+            eo[i] = noE ? 0.0 : ld_sub_msg(sub_es(c, eoff, i));
+            col[i] = lc[i];
         }
         const char *Lsrc = c.first ? c.Cu : c.Lu;  // iteration 0: M = ch (:85-90); uniform
 #pragma unroll
-        for (int i = 0; i < K; ++i)
-            if ((BF & 1) || i - i % kSG < rc.CS) t[i] = ld_l2((const double *)(Lsrc + sub_off(c, col[i])));
-        // tanh in groups of kSG slots evaluated in lockstep (np_tanh_n: the
-        // groups' table reads overlap); a group runs if its first slot is in
-        // the chunk (slots past CS hold clamped, valid data and end as 1.0)
+        for (int i = 0; i < K; ++i) t[i] = ld_l2((const double *)(Lsrc + sub_off(c, col[i])));
 #pragma unroll
-        for (int g0 = 0; g0 < K; g0 += kSG) {
-            if (LDPC_SUB_KDISP && kSG == 1 && g0 == K - 1 && rc.CS < K) {  // no piece reaches slot K-1
-                t[g0] = 1.0;
-                continue;
-            }
-            if ((BF & 1) || g0 < rc.CS) {
-                constexpr int G0 = kSG;
-                double d[G0];
-#pragma unroll
-                for (int q = 0; q < G0; ++q) {
-                    const int i = g0 + q < K ? g0 + q : K - 1;
-                    const double M = noE ? t[i] : t[i] - eo[i];  // :85-90 / :260-268
-                    d[q] = M * 0.5;
-                }
-                // :138-146 as np_tanh of M/2 clamped to +-17.5 (spa_math.h
-                // tanh_half_clipped: equal to the reference's clip for every M)
-                double th[G0];
-#pragma unroll
-                for (int q = 0; q < G0; ++q)
-                    th[q] = dfrom(dbits(fmin(fabs(d[q]), 17.5)) | (dbits(d[q]) & 0x8000000000000000ull));
-                np_tanh_n<G0, LdsTanh, true>(th, c.ttab);
-#pragma unroll
-                for (int q = 0; q < G0; ++q) {
-                    const int i = g0 + q;
-                    if (i < K) {
-                        const double tv = th[q];
-                        tiny |= i < njt && !(fabs(tv) > kTiny);
-                        // slots past this lane's piece: 1.0, an exact no-op in the chain product
-                        t[i] = i < nj ? tv : 1.0;
-                    }
-                }
-            }
+        for (int i = 0; i < K; ++i) {
+            const double M = noE ? t[i] : t[i] - eo[i];  // :85-90 / :260-268
+            const double d = M * 0.5;
+            // :138-146 as np_tanh of M/2 clamped to +-17.5 (spa_math.h
+            // tanh_half_clipped: equal to the reference's clip for every M)
+            double th[1] = {dfrom(dbits(fmin(fabs(d), 17.5)) | (dbits(d) & 0x8000000000000000ull))};
+            np_tanh_n<1, LdsTanh, true>(th, c.ttab);
+            const double tv = th[0];
+            tiny |= i < njt && !(fabs(tv) > kTiny);
+            // slots past this lane's piece: 1.0, an exact no-op in the chain product
+            t[i] = i < nj ? tv : 1.0;
         }
     }
     sub_stage_commit(c, r + 1, sv);
@@ -456,20 +361,11 @@ __device__ __forceinline__ void sub_hop(const SubCtx<Q> &c, int r, const double 
         // piece and every slot of a group past the chunk hold 1.0, sub_p1:
         // exact no-ops), so the product ends in group 3 -- no uniform
         // branches between the dependent multiplies
-        if (LDPC_SUB_KDISP && rc.CS < K) {  // slot K-1 holds 1.0 in every group: skip it
 #pragma unroll
-            for (int jj = 0; jj < Q; ++jj) {
+        for (int jj = 0; jj < Q; ++jj) {
 #pragma unroll
-                for (int i = 0; i < K - 1; ++i) P = P * t[i];
-                if (jj + 1 < Q) P = group_up4(P, jj);
-            }
-        } else {
-#pragma unroll
-            for (int jj = 0; jj < Q; ++jj) {
-#pragma unroll
-                for (int i = 0; i < K; ++i) P = P * t[i];
-                if (jj + 1 < Q) P = group_up4(P, jj);
-            }
+            for (int i = 0; i < K; ++i) P = P * t[i];
+            if (jj + 1 < Q) P = group_up4(P, jj);
         }
         last = Q - 1;
     } else {
@@ -499,7 +395,7 @@ __device__ __forceinline__ void sub_hop(const SubCtx<Q> &c, int r, const double 
 
 // P3: E_new of this lane's slots of row r, stored and folded into S; the
 // identity column's posterior and z^1 bit.
-template <int Q, int BF>
+template <int Q>
 __device__ __forceinline__ void sub_p3_body(SubCtx<Q> &c, int r, double (&t)[SubCfg<Q>::K]) {
     constexpr int F = SubCfg<Q>::F, K = SubCfg<Q>::K;
     const SubChunk rc = sub_chunk(c.row_ptr, r, c.wave, Q);
@@ -523,7 +419,7 @@ __device__ __forceinline__ void sub_p3_body(SubCtx<Q> &c, int r, double (&t)[Sub
     int col[K];
 #pragma unroll
     for (int i = 0; i < K; ++i)
-        if ((BF & 2) || i < rc.CS) col[i] = lc[i];  // clamped copy past the chunk: a valid column
+        col[i] = lc[i];  // clamped copy past the chunk: a valid column
     if (!tiny_row) {
         // q = P/t (div_nr: the IEEE quotient without the scaling steps,
         // cn_common.h), then E_new = 2 atanh(clip(q)) (:159-168) -- or 2q when
@@ -588,7 +484,7 @@ __device__ __forceinline__ void sub_p3_body(SubCtx<Q> &c, int r, double (&t)[Sub
             }
         }
     }
-    if (c.live && !LDPC_EXP_NOEST) {
+    if (c.live) {
         const uint32_t eoff = sub_eoff(c, rc);
 #pragma unroll
         for (int i = 0; i < K; ++i)
@@ -598,46 +494,20 @@ __device__ __forceinline__ void sub_p3_body(SubCtx<Q> &c, int r, double (&t)[Sub
     // lanes of a row share (col, frame)); the identity edge goes to `dummy`
     double EnI = 0.0;
     int colI = -1;
-    if constexpr ((BF & 2) != 0) {
-        double *sp[K];
-        double sv[K];
+    double *sp[K];
 #pragma unroll
-        for (int i = 0; i < K; ++i) {
-            const bool own = i < nj;  // nj <= CS
-            const bool a = own && col[i] < c.k;
-            sp[i] = a ? c.S + (size_t)col[i] * F : c.dummy;
-            if (own && !a) {
-                EnI = t[i];
-                colI = col[i];
-            }
-        }
-        if (LDPC_SUB_LDSADD) {  // A/B: one LDS fp64 atomic add per slot, no read round trip
-#pragma unroll
-            for (int i = 0; i < K; ++i)  // slots past the piece add into `dummy` (never read)
-                __hip_atomic_fetch_add(sp[i], t[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        } else {
-#pragma unroll
-            for (int i = 0; i < K; ++i) sv[i] = *sp[i];
-#pragma unroll
-            for (int i = 0; i < K; ++i) sv[i] = sv[i] + t[i];
-#pragma unroll
-            for (int i = 0; i < K; ++i) *sp[i] = sv[i];
-        }
-    } else {
-#pragma unroll
-        for (int i = 0; i < K; ++i) {
-            if (i < rc.CS) {
-                const bool own = i < nj;
-                const bool a = own && col[i] < c.k;
-                double *sp = a ? c.S + (size_t)col[i] * F : c.dummy;
-                *sp = *sp + t[i];
-                if (own && !a) {
-                    EnI = t[i];
-                    colI = col[i];
-                }
-            }
+    for (int i = 0; i < K; ++i) {
+        const bool own = i < nj;  // nj <= CS
+        const bool a = own && col[i] < c.k;
+        sp[i] = a ? c.S + (size_t)col[i] * F : c.dummy;
+        if (own && !a) {
+            EnI = t[i];
+            colI = col[i];
         }
     }
+#pragma unroll
+    for (int i = 0; i < K; ++i)  // one ds_add_f64 per slot; slots past the piece add into `dummy` (never read)
+        __hip_atomic_fetch_add(sp[i], t[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     if (colI >= 0) {  // identity column: L = ch + (0 + E) (:173-185)
         const double Lj = *sub_c(c, colI) + (0.0 + EnI);
         if (c.live) *sub_l(c, colI) = Lj;
@@ -659,13 +529,13 @@ __device__ __forceinline__ void sub_p3_body(SubCtx<Q> &c, int r, double (&t)[Sub
 // whose P3 wavefront v finished; sub_p3_reset zeroes it between passes (after
 // the barrier that ends a pass's rows), so the count never exceeds m + 1 however
 // many passes a streaming launch makes.
-template <int Q, int BF>
+template <int Q>
 __device__ __forceinline__ void sub_p3(SubCtx<Q> &c, int r, double (&t)[SubCfg<Q>::K]) {
     if (r > 0) {  // row r-1's P3 by the wavefronts whose column spans overlap ours
         const int d = c.p3dep[r * kSW + c.wave];
         for (int v = d & 0xff; v <= (d >> 8); ++v) wait_ge<false>(c.p3row + v, r);
     }
-    sub_p3_body<Q, BF>(c, r, t);
+    sub_p3_body<Q>(c, r, t);
     lds_release();  // this row's S additions before the count
     if ((threadIdx.x & 63) == 0)
         lds_st(c.p3row + c.wave, r + 1);
@@ -681,12 +551,12 @@ __device__ __forceinline__ int sub_epoch0(int pass, int m) {
     return (int)(((uint32_t)pass * (uint32_t)m) & 0x3ffffffu);
 }
 
-template <int Q, int BF>
+template <int Q>
 __device__ __forceinline__ void sub_body(SubCtx<Q> &c, int r, int m, double (&tcur)[SubCfg<Q>::K], bool ycur,
                                          double (&toth)[SubCfg<Q>::K], bool &yoth) {
     if (r < m) sub_hop(c, r, tcur, ycur);
-    if (r >= 1) sub_p3<Q, BF>(c, r - 1, toth);
-    if (r + 1 < m) yoth = sub_p1<Q, BF>(c, r + 1, sub_chunk(c.row_ptr, r + 1, c.wave, Q), toth);
+    if (r >= 1) sub_p3<Q>(c, r - 1, toth);
+    if (r + 1 < m) yoth = sub_p1<Q>(c, r + 1, sub_chunk(c.row_ptr, r + 1, c.wave, Q), toth);
 }
 
 template <int Q>
@@ -730,7 +600,6 @@ __global__ __launch_bounds__(64 * kSW, 1) void tile_sub_kernel(DevGraph g, DevSt
 
     SubCtx<Q> c;
     c.col_idx = col_idx;
-    c.col16 = g.col16;
     c.row_ptr = row_ptr;
     const size_t lo = (size_t)sub * F + f;
     c.Eb = st.E + (size_t)tile * g.nnz * kTile + lo;
@@ -751,7 +620,7 @@ __global__ __launch_bounds__(64 * kSW, 1) void tile_sub_kernel(DevGraph g, DevSt
     c.tinyf = flags + kSR;
     c.tseq = flags + 2 * kSR;
     c.p3row = flags + 2 * kSR + 2;
-    c.p3dep = kSW == 12 ? g.p3dep12 : g.p3dep;
+    c.p3dep = g.p3dep;
     c.ttab = LdsTanh{mlds.tanh};
     c.ltab = LdsAtanh{mlds.atanh};
     c.ac = ac;
@@ -773,11 +642,11 @@ __global__ __launch_bounds__(64 * kSW, 1) void tile_sub_kernel(DevGraph g, DevSt
         bool yA = false, yB = false;
         if (m > 0) {
             sub_stage_commit(c, 0, sub_stage_issue(c, 0));
-            yA = sub_p1<Q, kStaticBF>(c, 0, sub_chunk(row_ptr, 0, wave, Q), tA);
+            yA = sub_p1<Q>(c, 0, sub_chunk(row_ptr, 0, wave, Q), tA);
         }
         for (int r = 0; r <= m; r += 2) {
-            sub_body<Q, kStaticBF>(c, r, m, tA, yA, tB, yB);
-            if (r + 1 <= m) sub_body<Q, kStaticBF>(c, r + 1, m, tB, yB, tA, yA);
+            sub_body<Q>(c, r, m, tA, yA, tB, yB);
+            if (r + 1 <= m) sub_body<Q>(c, r + 1, m, tB, yB, tA, yA);
         }
         __syncthreads();  // every P3 done: S complete, identity bits set
         sub_p3_reset(c.p3row);
@@ -902,7 +771,6 @@ __global__ __launch_bounds__(64 * kSW, 1) void tile_sub_stream_kernel(
 
     SubCtx<Q> c;
     c.col_idx = col_idx;
-    c.col16 = g.col16;
     c.row_ptr = row_ptr;
     const size_t lo = (size_t)lane64;
     c.Eb = st.E + (size_t)tile * g.nnz * kTile + lo;
@@ -923,7 +791,7 @@ __global__ __launch_bounds__(64 * kSW, 1) void tile_sub_stream_kernel(
     c.tinyf = flags + kSR;
     c.tseq = flags + 2 * kSR;
     c.p3row = flags + 2 * kSR + 2;
-    c.p3dep = kSW == 12 ? g.p3dep12 : g.p3dep;
+    c.p3dep = g.p3dep;
     c.ttab = LdsTanh{mlds.tanh};
     c.ltab = LdsAtanh{mlds.atanh};
     c.ac = ac;
@@ -997,11 +865,11 @@ __global__ __launch_bounds__(64 * kSW, 1) void tile_sub_stream_kernel(
         bool yA = false, yB = false;
         if (m > 0) {
             sub_stage_commit(c, 0, sub_stage_issue(c, 0));
-            yA = sub_p1<Q, kStreamBF>(c, 0, sub_chunk(row_ptr, 0, wave, Q), tA);
+            yA = sub_p1<Q>(c, 0, sub_chunk(row_ptr, 0, wave, Q), tA);
         }
         for (int r = 0; r <= m; r += 2) {
-            sub_body<Q, kStreamBF>(c, r, m, tA, yA, tB, yB);
-            if (r + 1 <= m) sub_body<Q, kStreamBF>(c, r + 1, m, tB, yB, tA, yA);
+            sub_body<Q>(c, r, m, tA, yA, tB, yB);
+            if (r + 1 <= m) sub_body<Q>(c, r + 1, m, tB, yB, tA, yA);
         }
         __syncthreads();
         sub_p3_reset(c.p3row);

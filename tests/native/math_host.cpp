@@ -10,14 +10,6 @@ extern "C" void host_atanh(const double *x, double *y, long n) {
     ldpc::HostAtanhTab t;
     for (long i = 0; i < n; ++i) y[i] = ldpc::atanh_f(x[i], t);
 }
-extern "C" void host_atanh_tab(const double *x, double *y, long n) {  // the LDPC_ATANH_TAB=1 form
-    ldpc::HostAtabTab t;
-    for (long i = 0; i < n; ++i) {
-        const double a = x[i] < 0 ? -x[i] : x[i];
-        const double r = a < ldpc::kAtanhSmall ? ldpc::atanh_small_abs(a) : ldpc::atanh_tab_abs(a, t, ldpc::kAtanhCoef);
-        y[i] = x[i] < 0 ? -r : r;
-    }
-}
 extern "C" void host_log(const double *x, double *y, long n) {
     ldpc::HostLogTab t;
     for (long i = 0; i < n; ++i) {

@@ -13,13 +13,7 @@
    written (tests/test_math.py re-checks on every CPU run).
 
 2. A 128-entry natural-log table (invc, -log(invc) as a double-double) for the
-   decoder's log-based atanh (the LDPC_ATANH_TAB=0 form), computed with `decimal`.
-
-3. A 216-entry atanh table for the decoder's default atanh (LDPC_ATANH_TAB=1,
-   spa_math.h atanh_tab_abs): atanh(c_i) as a double-double at the centres
-   c_i of 4 sub-intervals per binade -- of a itself for 2^-5 <= a <= 1/2
-   (entries 0..19), of v = 1 - a for a > 1/2 (entries 20..215, v down to
-   1 - CL > 2^-50) -- computed with `decimal` at 90 digits.
+   decoder's log-based atanh (spa_math.h atanh_f), computed with `decimal`.
 
 Usage: python tools/gen_tables.py   (rewrites the two headers below)
 """
@@ -131,34 +125,11 @@ def log_table(nbits=7):
     return rows
 
 
-def atanh_table():
-    """kAtab[i] = {hi, lo}: atanh(c_i) = hi + lo (hi = the double nearest)."""
-    getcontext().prec = 90
-
-    def d(u):
-        return struct.unpack("<d", struct.pack("<Q", u))[0]
-
-    rows = []
-    for idx in range(216):
-        region2 = idx >= 20
-        j = idx - 20 if region2 else idx
-        ef = (973 if region2 else 1018) + j // 4
-        xi = d((ef << 52) | ((j % 4) << 50) | (1 << 49))  # centre: 2^e (1 + m/4 + 1/8)
-        c = 1 - Decimal(xi) if region2 else Decimal(xi)
-        if region2:
-            assert Decimal(1.0 - xi) == c  # 1 - x_i is exact in double (x_i >= 2^-50, 5 bits)
-        T = ((1 + c) / (1 - c)).ln() / 2
-        hi = float(T)
-        rows.append((hi, float(T - Decimal(hi))))
-    return rows
-
-
 def main():
     b, cs = find_numpy_tanh_table()
     n = verify(b, cs)
     print(f"numpy tanh restatement verified bit-exact on {n} inputs")
     logt = log_table()
-    atab = atanh_table()
 
     def hx(u):
         return "0x%016xULL" % u
@@ -171,8 +142,7 @@ def main():
         "// (1) numpy 2.2.6 float64 tanh coefficient table (loops_hyperbolic, AVX512_SKX",
         "//     dispatch): kTanhB[i] = interval base b, kTanhC[p][i] = coefficient of y^p,",
         "//     y = |x| - b.  Restated algorithm verified bit-exact against np.tanh.",
-        "// (2) log table for the decoder's log-based atanh (LDPC_ATANH_TAB=0): 128 x {invc, -log(invc) hi, lo}.",
-        "// (3) atanh table for the default atanh (LDPC_ATANH_TAB=1): 216 x {atanh(c_i) hi, lo}.",
+        "// (2) log table for the decoder's log-based atanh: 128 x {invc, -log(invc) hi, lo}.",
         "#pragma once",
         "#include <cstdint>",
         "namespace ldpc {",
@@ -186,10 +156,6 @@ def main():
     hdr.append("constexpr uint64_t kLog[128][3] = {  // invc, logc_hi, logc_lo")
     for invc, h, lo in logt:
         hdr.append("    {%s, %s, %s}," % (hx(dbits(invc)), hx(dbits(h)), hx(dbits(lo))))
-    hdr.append("};")
-    hdr.append("constexpr uint64_t kAtab[216][2] = {  // atanh(c_i) hi, lo")
-    for h, lo in atab:
-        hdr.append("    {%s, %s}," % (hx(dbits(h)), hx(dbits(lo))))
     hdr.append("};")
     hdr.append("}  // namespace tab")
     hdr.append("}  // namespace ldpc")
