@@ -395,13 +395,15 @@ int run_iterations(ldpc_decoder *d, const DevGraph &G, const DevState &st_in, in
 
 // cn_rare_kernel runs 1024 blocks x 4 wavefronts; one scratch slot each.
 int scratch_slots() { return 4096; }
+// scratch slots (max_row_deg x 64 doubles) per tile the tile decoders need
+int tile_scratch_rows(const DevGraph &g) { return g.ef == 8 ? ldpc::tile8_scratch_per_tile(g) : 1; }
 
 size_t workspace_bytes(const DevGraph &g, int cap_tiles) {
     const size_t cap = (size_t)cap_tiles * kTile;
     const size_t kw = (size_t)((g.k + 31) / 32);
     size_t b = 0;
     b += cap * (size_t)g.nnz * 8;                                   // E
-    const size_t slots = ldpc::use_tile(g) ? std::max(scratch_slots(), cap_tiles) : scratch_slots();
+    const size_t slots = ldpc::use_tile(g) ? std::max(scratch_slots(), cap_tiles * tile_scratch_rows(g)) : scratch_slots();
     b += slots * g.max_row_deg * kTile * 8;  // T pool
     b += 4 * (2 + (size_t)cap_tiles * g.m * 4);                           // rare list
     b += 2 * cap * (size_t)g.n * 8;    // L, ch
@@ -549,6 +551,11 @@ int ldpc_graph_create(int32_t m, int32_t n, const int32_t *row_ptr, const int32_
     }
     // the WiMAX 2304 codes run the 8-frame sub-tile decoder: E in 8-frame blocks
     if (e == hipSuccess && !ldpc::tile64_lds_bytes(G) && ldpc::tile8_applies(G)) G.ef = 8;
+    // its pair form (two rows per wavefront): LDPC_T8_PAIR=1 (A/B)
+    if (G.ef == 8 && ldpc::tile8_pair_fits(G)) {
+        const char *ep = getenv("LDPC_T8_PAIR");
+        G.t8pair = ep && atoi(ep) != 0 ? 1 : 0;
+    }
     if (e != hipSuccess) {
         (void)hipFree(g->d_ints);
         (void)hipFree(g->d_apack);
@@ -624,7 +631,8 @@ int ldpc_decoder_create(const ldpc_graph *g, int32_t max_frames, ldpc_decoder **
     const size_t kw = (size_t)((G.k + 31) / 32);
     int rc = LDPC_OK;
     d->nslots = scratch_slots();  // E and T are allocated on first parity-mode use
-    if (ldpc::use_tile(G)) d->nslots = std::max(d->nslots, d->cap_tiles);  // one scratch slot per tile workgroup
+    if (ldpc::use_tile(G))  // one scratch row per tile workgroup (two for tile8's pair form)
+        d->nslots = std::max(d->nslots, d->cap_tiles * tile_scratch_rows(G));
     // rare list: one entry per (tile, row), or per 16-frame sub-tile of it (cn_sub_kernel);
     // entries pack tile * m + row into 28 bits (spa_device.h rare_code)
     if ((int64_t)d->cap_tiles * G.m >= (int64_t)1 << 28) {

@@ -43,6 +43,7 @@ struct DevGraph {
     const int *p3dep;          // [m][16] sub-tile S order: lo | hi << 8 (tile_sub.hip sub_p3)
     const int *p3dep8;         // [m][16] the same over each row's A edges (tile8.hip: identity excluded)
     int ef;                    // frames per E block (64, or 8 for tile8.hip's graphs): e_base
+    int t8pair;                // tile8.hip runs its pair form (two rows per wavefront) on this graph
 };
 
 // E layout inside a tile: the 64 frames in blocks of g.ef, each block
@@ -113,7 +114,11 @@ hipError_t launch_tile_stream(const DevGraph &g, const DevState &st, int max_ite
 // 8-frame sub-tile decoder (tile8.hip): the WiMAX 2304 codes; its graphs keep
 // E in 8-frame blocks (DevGraph::ef = 8, chosen at graph creation)
 bool tile8_applies(const DevGraph &g);
+// whether tile8.hip's pair form can run this graph (set DevGraph::t8pair from it at graph creation)
+bool tile8_pair_fits(const DevGraph &g);
 size_t tile8_lds_bytes(const DevGraph &g);
+// rare-row scratch rows per tile it needs (1, or 2 for its pair form)
+int tile8_scratch_per_tile(const DevGraph &g);
 hipError_t launch_tile8(const DevGraph &g, const DevState &st, int max_iter, bool nllr, hipStream_t s);
 // its streaming Monte-Carlo form (one persistent launch per SNR point, handoff as launch_tile_stream)
 size_t tile8_stream_lds_bytes(const DevGraph &g);

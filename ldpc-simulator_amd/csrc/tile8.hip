@@ -169,6 +169,7 @@ struct T8Ctx {
     LdsAtanh ltab;
     AtanhCoef ac;
     int m, k, wave, j, f;
+    int h;  // pair form: this lane's row of the pair (lane = h*32 + j*8 + f); 0 otherwise
     int ep0;
     bool first, live, fresh;
     int ntiny;
@@ -582,7 +583,367 @@ __device__ __forceinline__ void t8_rows(T8Ctx<K> &c) {
     }
 }
 
-template <int K, bool LA>
+// ---------------------------------------------------------------------------
+// Pair form: TWO rows per wavefront.  lane = h*32 + j*8 + f: half h carries row
+// 2q + h of row pair q, in 4 lane groups j of the 8 frames f.  A row's A edges
+// are chunked over the 16 wavefronts exactly as above (C = ceil((deg-1)/16):
+// p3dep8 applies unchanged) and a chunk over 4 lane-group pieces of
+// CS = ceil(C/4) <= K edges, so one wavefront instruction covers 64 lane-edges
+// with 4 groups per row -- tile_sub.hip's instruction shape (its 16 frames x 4
+// groups) on the 8-frame layout that keeps the column sums AND the A-column
+// posteriors in LDS: P1 reads L[col] from LDS instead of gathering it from L2
+// (the 8-frame decoder above pays 8 lane groups per row for that, 117 VALU per
+// wave slot against tile_sub's 83, profiles/r5a_counters).  Both rows' products
+// run in the same instructions: each half hands its running product group to
+// group (DPP row_shr / row_ror + permlane16) and wavefront to wavefront through
+// its own LDS slot.  P3 adds half 0's E_new (row 2q), publishes, then half 1's
+// (row 2q+1) after the overlapping wavefronts' row 2q: the rows-ascending order
+// of every column sum.  Pipeline body(q) = hop(q), P3(q-1), P1(q+1); the column
+// indices of pair q+1 are staged during P3(q-1) into the ring row P3(q-1) has
+// just read (2 ring rows).  Chain slots: kPSR pairs x 2 halves in the same LDS
+// as the row form's kSR8 rows.
+constexpr int kPQ = 4;    // lane groups per row
+constexpr int kPSR = 4;   // chain slots (pairs): a slot is reused after every P3 of its pair (idwave = last)
+static_assert(2 * kPSR <= kSR8, "pair chain slots share the row form's LDS");
+
+struct PChunk {
+    int deg, beg, c0, cnt, CS;  // this lane's row (per half)
+    int cs_max;                 // max CS over the two rows (uniform)
+    bool any;                   // some chunk of this wavefront has edges (uniform)
+};
+template <int K>
+__device__ __forceinline__ PChunk tp_chunk(const T8Ctx<K> &c, int q) {
+    const int r0 = 2 * q;
+    // uniform (scalar) loads; rows >= m are empty
+    const int b0 = c.row_ptr[min(r0, c.m)], b1 = c.row_ptr[min(r0 + 1, c.m)], b2 = c.row_ptr[min(r0 + 2, c.m)];
+    const int da0 = max(b1 - b0 - 1, 0), da1 = max(b2 - b1 - 1, 0);
+    const int C0 = (da0 + kW8 - 1) / kW8, C1 = (da1 + kW8 - 1) / kW8;
+    const int n0 = max(0, min(da0 - c.wave * C0, C0)), n1 = max(0, min(da1 - c.wave * C1, C1));
+    PChunk rc;
+    rc.beg = c.h ? b1 : b0;
+    rc.deg = (c.h ? b2 : b1) - rc.beg;
+    const int C = c.h ? C1 : C0;
+    rc.c0 = rc.beg + c.wave * C;
+    rc.cnt = c.h ? n1 : n0;
+    rc.CS = (C + kPQ - 1) / kPQ;
+    rc.cs_max = (max(C0, C1) + kPQ - 1) / kPQ;
+    rc.any = n0 > 0 || n1 > 0;
+    return rc;
+}
+template <int K>
+__device__ __forceinline__ int tp_nj(const T8Ctx<K> &c, const PChunk &rc) {
+    return max(0, min(rc.cnt - c.j * rc.CS, rc.CS));
+}
+// ring row q%2: half h's 4K positions at [h * 4K], this lane's slot i at [j*CS + i]
+template <int K>
+__device__ __forceinline__ const uint16_t *tp_lcols(const T8Ctx<K> &c, int q, const PChunk &rc) {
+    return c.cidx + (q & 1) * kW8 * 8 * K + c.h * kPQ * K + c.j * rc.CS;
+}
+// Staging of pair q's indices: lane L takes position L of both rows' chunks
+// (clamped to the chunk's last edge; rows past the chunk: 0).
+struct TpStage {
+    int v0, v1;
+};
+template <int K>
+__device__ __forceinline__ TpStage tp_stage_issue(const T8Ctx<K> &c, int q) {
+    TpStage v{0, 0};
+    if (2 * q >= c.m) return v;
+    const int r0 = 2 * q;
+    const int b0 = c.row_ptr[r0], b1 = c.row_ptr[min(r0 + 1, c.m)], b2 = c.row_ptr[min(r0 + 2, c.m)];
+    const int da0 = max(b1 - b0 - 1, 0), da1 = max(b2 - b1 - 1, 0);
+    const int C0 = (da0 + kW8 - 1) / kW8, C1 = (da1 + kW8 - 1) / kW8;
+    const int n0 = max(0, min(da0 - c.wave * C0, C0)), n1 = max(0, min(da1 - c.wave * C1, C1));
+    const int L = threadIdx.x & 63;
+    if (n0 > 0) v.v0 = c.col_idx[b0 + c.wave * C0 + min(L, n0 - 1)];
+    if (n1 > 0) v.v1 = c.col_idx[b1 + c.wave * C1 + min(L, n1 - 1)];
+    return v;
+}
+template <int K>
+__device__ __forceinline__ void tp_stage_commit(const T8Ctx<K> &c, int q, TpStage v) {
+    if (2 * q >= c.m) return;
+    constexpr int W = kPQ * K;  // positions per row chunk
+    const int L = threadIdx.x & 63;
+    uint16_t *ring = c.cidx + (q & 1) * kW8 * 8 * K;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    if (L < W) {
+        ring[L] = (uint16_t)v.v0;
+        ring[W + L] = (uint16_t)v.v1;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// P1 of pair q: t = tanh((L[col] - E_old)/2) of this lane's slots (L_A from
+// LDS); the identity edges' t (idwave) published in the pair's slot.  Returns
+// the rows' |t| <= 1e-10 votes: bit h = some live lane of half h.
+template <int K>
+__device__ __forceinline__ int tp_p1(const T8Ctx<K> &c, int q, double (&t)[K]) {
+    const PChunk rc = tp_chunk(c, q);
+    bool tiny = false;
+    const int nj = tp_nj(c, rc);
+    const int njt = c.live ? nj : 0;  // frame-less lanes abstain
+    if (rc.any) {
+        const uint16_t *lc = tp_lcols(c, q, rc);
+        const uint32_t eoff = ((uint32_t)(rc.c0 + c.j * rc.CS) << 6) + c.eo8;
+        const bool noE = c.first || c.fresh;  // M = L - 0.0 == L: no E_old
+        // E_old straight into t (all slots in flight); L[col] from LDS just
+        // before each slot's tanh (short latency: no second array of loads)
+#pragma unroll
+        for (int i = 0; i < K; ++i) t[i] = noE ? 0.0 : t8_ld<kNT>(c.rE, t8_es(c, eoff, i));
+        const bool skip_last = rc.cs_max < K;  // wave-uniform: no piece reaches slot K-1
+#pragma unroll
+        for (int i = 0; i < K; ++i) {
+            if (i == K - 1 && skip_last) {
+                t[i] = 1.0;
+                continue;
+            }
+            const double Lc = c.LA[(size_t)lc[i] * kF8];   // L[col] (LDS)
+            const double M = noE ? Lc : Lc - t[i];  // :85-90 / :260-268
+            const double tv = tanh_half_clipped(M, c.ttab);  // :138-146
+            tiny |= i < njt && !(fabs(tv) > kTiny);
+            t[i] = i < nj ? tv : 1.0;  // past the piece: an exact no-op in the product
+        }
+    } else {
+#pragma unroll
+        for (int i = 0; i < K; ++i) t[i] = 1.0;
+    }
+    if (c.wave == c.idwave) {  // the identity edges k + 2q + h (a fresh frame has L = ch: gen_slots)
+        const int r = 2 * q + c.h;
+        if (rc.deg > 0) {
+            const bool noE = c.first || c.fresh;
+            const double lid = t8_ld(c.first ? c.rC : c.rL, ((uint32_t)(c.k + r) << 9) + c.lo8);
+            const double eid = noE ? 0.0 : t8_ld<kNT>(c.rE, ((uint32_t)(rc.beg + rc.deg - 1) << 6) + c.eo8);
+            const double tv = tanh_half_clipped(noE ? lid : lid - eid, c.ttab);
+            tiny |= c.live && !(fabs(tv) > kTiny);
+            if (c.j == 0) c.slot[(kSR8 + (q & (kPSR - 1)) * 2 + c.h) * kF8] = tv;
+        }
+    }
+    const unsigned long long b = __ballot(tiny);
+    return ((uint32_t)b != 0u ? 1 : 0) | ((b >> 32) != 0ull ? 2 : 0);
+}
+
+// hop of pair q: this wavefront's chunks of both rows' left-to-right products.
+template <int K>
+__device__ __forceinline__ void tp_hop(T8Ctx<K> &c, int q, const double (&t)[K], int tiny) {
+    const int s = q & (kPSR - 1);
+    const int ep = ((c.ep0 + q) & 0x3ffffff) * 32;
+    double *sl = c.slot + (s * 2 + c.h) * kF8;
+    double P = 1.0;  // 1.0 * t0 == t0 exactly
+    if (c.wave != 0) {
+        wait_flag<false>(c.flag + s, ep + c.wave);
+        P = *sl;
+    }
+    __builtin_amdgcn_s_setprio(2);
+    if (uniform(tp_chunk(c, q).any ? 1 : 0)) {
+        // branch-free: every group multiplies all K slots (1.0-padded: exact
+        // no-ops), the running product moves group j -> j+1 inside each half
+        // (t8_up's first three steps), so it ends in group 3 of each half
+#pragma unroll
+        for (int jj = 0; jj < kPQ; ++jj) {
+#pragma unroll
+            for (int i = 0; i < K; ++i) P = P * t[i];
+            if (jj + 1 < kPQ) P = t8_group_up(P, jj);
+        }
+    }
+    if ((threadIdx.x & 63) == 0) {
+        if (c.wave == 0) {
+            lds_st(c.tinyf + s * 2, tiny & 1);
+            lds_st(c.tinyf + s * 2 + 1, tiny >> 1);
+        } else {
+            if (tiny & 1) lds_st(c.tinyf + s * 2, 1);
+            if (tiny & 2) lds_st(c.tinyf + s * 2 + 1, 1);
+        }
+    }
+    if (c.j == kPQ - 1) *sl = P;
+    lds_release();
+    if ((threadIdx.x & 63) == 0) lds_st(c.flag + s, ep + c.wave + 1);
+    __builtin_amdgcn_s_setprio(0);
+}
+
+// Row r's S additions may start once the wavefronts whose column spans
+// overlap this one's have added row r-1 (p3row[v] = 1 + their last row).
+template <int K>
+__device__ __forceinline__ void tp_order(const T8Ctx<K> &c, int r) {
+    if (r > 0 && r < c.m) {
+        const int d = c.p3dep[r * kW8 + c.wave];
+        for (int v = d & 0xff; v <= (d >> 8); ++v) wait_ge<false>(c.p3row + v, r);
+    }
+}
+
+// P3 of pair q: E_new of this lane's slots (:159-168), stored; S_col += E_new
+// row 2q then row 2q+1 in the column order; the identity columns' posteriors
+// and z^1 bits.  The indices of pair q+2 (staged by the caller) replace this
+// pair's ring row once read.
+template <int K>
+__device__ __forceinline__ void tp_p3(T8Ctx<K> &c, int q, double (&t)[K], TpStage nxt) {
+    const PChunk rc = tp_chunk(c, q);
+    const int s = q & (kPSR - 1);
+    const int ep = ((c.ep0 + q) & 0x3ffffff) * 32;
+    const int r = 2 * q + c.h;
+    const bool idw = c.wave == c.idwave && rc.deg > 0;  // this lane holds its row's identity edge
+    double chI = 0.0;
+    if (idw) chI = t8_ld(c.rC, ((uint32_t)(c.k + r) << 9) + c.lo8);  // for L = ch + (0 + E)
+    int col[K];
+    {
+        const uint16_t *lc = tp_lcols(c, q, rc);
+#pragma unroll
+        for (int i = 0; i < K; ++i) col[i] = lc[i];
+    }
+    tp_stage_commit(c, q + 2, nxt);  // the ring row is read (in-order LDS of this wavefront)
+    wait_flag<false>(c.flag + s, ep + kW8);  // both rows' A products are complete
+    const bool tiny_row = lds_ld(c.tinyf + s * 2 + c.h) != 0;
+    const bool tiny_any = __ballot(tiny_row) != 0ull;
+    const int nj = tp_nj(c, rc);
+    const double tI = c.slot[(kSR8 + s * 2 + c.h) * kF8];
+    const double P = c.slot[(s * 2 + c.h) * kF8] * tI;  // (t_0 * ... * t_{deg-2}) * t_id: left to right
+    // E_new stored (slots past the piece and frames that stopped store out of
+    // range: dropped); S_col += E_new row 2q then row 2q+1 in the column
+    // order; the identity columns.  Called at the end of each branch so the
+    // branches' E_new values never merge (a merge cost ~200 spilled VGPRs).
+    auto finish = [&](double (&tt)[K], double EI) {
+        {  // slots past the piece (and frames that stopped) store out of range: dropped
+            const uint32_t eoff = ((uint32_t)(rc.c0 + c.j * rc.CS) << 6) + c.eo8;
+#pragma unroll
+            for (int i = 0; i < K; ++i) t8_st<kEStAux>(c.rE, (i < nj && c.live) ? t8_es(c, eoff, i) : kOOB, tt[i]);
+            if (idw && c.j == 0 && c.live) t8_st<kEStAux>(c.rE, ((uint32_t)(rc.beg + rc.deg - 1) << 6) + c.eo8, EI);
+        }
+        // S_col += E_new; slots past the piece add into `dummy` (never read)
+        auto sp = [&](int i) { return i < nj ? c.S + (size_t)col[i] * kF8 : c.dummy; };
+        // row 2q: half 0's additions after the overlapping wavefronts' row 2q-1
+        tp_order(c, 2 * q);
+        if (c.h == 0) {
+#pragma unroll
+            for (int i = 0; i < K; ++i) __hip_atomic_fetch_add(sp(i), tt[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+        lds_release();
+        if ((threadIdx.x & 63) == 0) lds_st(c.p3row + c.wave, 2 * q + 1);
+        // row 2q+1: half 1's, after the overlapping wavefronts' row 2q
+        tp_order(c, 2 * q + 1);
+        if (c.h == 1) {
+#pragma unroll
+            for (int i = 0; i < K; ++i) __hip_atomic_fetch_add(sp(i), tt[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+        if (idw && c.j == 0) {  // identity column: L = ch + (0 + E) (:173-185)
+            const double Lj = chI + (0.0 + EI);
+            if (c.live) t8_st(c.rL, ((uint32_t)(c.k + r) << 9) + c.lo8, Lj);
+            if (!(Lj < 0.0)) atomicOr(c.ib + (r >> 5) * kF8, 1u << (r & 31));
+        }
+        lds_release();
+        if ((threadIdx.x & 63) == 0) lds_st(c.p3row + c.wave, 2 * q + 2);
+    };
+    if (!tiny_any) {
+        // q = P/t (div_nr where exact), then E_new = 2 atanh(clip(q)), or 2q
+        // when every quotient of the wavefront is below 2^-27 (exact).
+        // Branch-free over all K slots (a padded slot's t = 1.0 gives q = P):
+        // per-slot uniform branches made the slots' values merge from many
+        // paths (~200 spilled VGPRs).
+        const bool dnr = div_nr_ok(c.live ? P : 1.0);
+        bool big = false;  // frame-less lanes do not vote
+        const double tIx = idw ? tI : 1.0;
+        double EI;
+        if (dnr) {
+#pragma unroll
+            for (int i = 0; i < K; ++i) t[i] = div_nr(P, t[i]);
+            EI = div_nr(P, tIx);
+        } else {
+#pragma unroll
+            for (int i = 0; i < K; ++i) t[i] = P / t[i];
+            EI = P / tIx;
+        }
+#pragma unroll
+        for (int i = 0; i < K; ++i) big |= !(fabs(t[i]) < kAtanhIdent);
+        big |= idw && !(fabs(EI) < kAtanhIdent);
+        if (__ballot(big && c.live) == 0ull) {
+#pragma unroll
+            for (int i = 0; i < K; ++i) t[i] = 2.0 * t[i];
+            EI = 2.0 * EI;
+        } else {
+#pragma unroll
+            for (int i = 0; i < K; ++i) t[i] = 2.0 * atanh_f(clip_cl(t[i]), c.ltab, c.ac);
+            EI = 2.0 * atanh_f(clip_cl(EI), c.ltab, c.ac);
+        }
+        finish(t, EI);
+    } else {
+        double EI = 0.0;
+        // rare: q = in-order product of the others (np.prod(np.delete(...)),
+        // :164) for an edge with |t| <= 1e-10 of a tiny row; t parked at row
+        // positions (the identity edge at deg-1), every wavefront counts
+        const int pos0 = rc.c0 + c.j * rc.CS - rc.beg;
+        if (tiny_row) {
+#pragma unroll
+            for (int i = 0; i < K; ++i)
+                if (i < nj) c.Tb[(size_t)(pos0 + i) * kF8] = t[i];
+            if (idw && c.j == 0) c.Tb[(size_t)(rc.deg - 1) * kF8] = tI;
+        }
+        __builtin_amdgcn_s_waitcnt(0);  // scratch stores have reached L2
+        c.ntiny += 1;
+        if ((threadIdx.x & 63) == 0) __hip_atomic_fetch_add(c.tseq, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        wait_flag<false>(c.tseq, c.ntiny * kW8);
+        auto others = [&](int pos) {
+            double qq = 1.0;
+            bool fst = true;
+            for (int p = 0; p < rc.deg; ++p) {
+                if (p == pos) continue;
+                const double t2 = ld_l2(c.Tb + (size_t)p * kF8);
+                qq = fst ? t2 : qq * t2;
+                fst = false;
+            }
+            return qq;
+        };
+        // Every live lane's own slots go through E (their E_old is consumed:
+        // E is this pass's scratch until E_new lands there), so ONE rolled
+        // loop -- one copy of atanh and of the product loop, not K -- turns
+        // each into E_new: q = P/t, or for a tiny t of a tiny row the product
+        // of the others; then the slots come back into registers.
+        const uint32_t eoff = ((uint32_t)(rc.c0 + c.j * rc.CS) << 6) + c.eo8;
+#pragma unroll
+        for (int i = 0; i < K; ++i) t8_st<kEStAux>(c.rE, (i < nj && c.live) ? t8_es(c, eoff, i) : kOOB, t[i]);
+        __builtin_amdgcn_s_waitcnt(0);  // this lane's stores are visible to its own loads
+#pragma unroll 1
+        for (int i = 0; i < nj; ++i) {
+            if (c.live) {
+                const double ti = t8_ld(c.rE, t8_es(c, eoff, i));
+                const double qv = (tiny_row && !(fabs(ti) > kTiny)) ? others(pos0 + i) : P / ti;
+                t8_st<kEStAux>(c.rE, t8_es(c, eoff, i), 2.0 * atanh_f(clip_cl(qv), c.ltab, c.ac));
+            }
+        }
+        if (idw) {
+            const double qv = (!tiny_row || fabs(tI) > kTiny) ? P / tI : others(rc.deg - 1);
+            EI = 2.0 * atanh_f(clip_cl(qv), c.ltab, c.ac);
+        }
+        __builtin_amdgcn_s_waitcnt(0);
+#pragma unroll
+        for (int i = 0; i < K; ++i)
+            t[i] = t8_ld(c.rE, (i < nj && c.live) ? t8_es(c, eoff, i) : kOOB);  // past the piece: 0 (unused)
+        finish(t, EI);
+    }
+}
+
+// body(q) = hop(q), P3(q-1) (staging pair q+1), P1(q+1)
+template <int K>
+__device__ __forceinline__ void tp_body(T8Ctx<K> &c, int q, int mp, double (&tc)[K], int yc, double (&to)[K],
+                                        int &yo) {
+    if (q < mp) tp_hop(c, q, tc, yc);
+    if (q >= 1) tp_p3(c, q - 1, to, tp_stage_issue(c, q + 1));
+    if (q + 1 < mp) yo = tp_p1(c, q + 1, to);
+}
+
+// One pass over all row pairs (every P3 done on return, before the barrier).
+template <int K>
+__device__ __forceinline__ void tp_rows(T8Ctx<K> &c) {
+    const int mp = (c.m + 1) / 2;  // pairs (an odd m's last pair has an empty second row)
+    if (mp <= 0) return;
+    double tA[K], tB[K];
+    int yA = 0, yB = 0;
+    tp_stage_commit(c, 0, tp_stage_issue(c, 0));
+    tp_stage_commit(c, 1, tp_stage_issue(c, 1));
+    yA = tp_p1(c, 0, tA);
+    for (int q = 0; q <= mp; q += 2) {
+        tp_body(c, q, mp, tA, yA, tB, yB);
+        if (q + 1 <= mp) tp_body(c, q + 1, mp, tB, yB, tA, yA);
+    }
+}
+
+template <int K, bool LA, bool PAIR>
 __device__ __forceinline__ void t8_setup(T8Ctx<K> &c, unsigned char *lds, const T8Layout &ly, const DevGraph &g,
                                          const DevState &st, int tile, int sub, const int *col_idx,
                                          const int *row_ptr, const AtanhCoef &ac) {
@@ -593,7 +954,8 @@ __device__ __forceinline__ void t8_setup(T8Ctx<K> &c, unsigned char *lds, const 
     c.row_ptr = row_ptr;
     c.p3dep = g.p3dep8;
     c.wave = uniform(t8_wave(threadIdx.x >> 6));
-    c.j = lane >> 3;
+    c.j = PAIR ? (lane >> 3) & 3 : lane >> 3;
+    c.h = PAIR ? lane >> 5 : 0;
     c.f = lane & 7;
     c.rE = t8_rsrc(st.E + (size_t)tile * g.nnz * kTile + (size_t)sub * g.nnz * kF8,
                    ((size_t)g.nnz + kEPadEdges) * kF8 * sizeof(double));
@@ -601,7 +963,9 @@ __device__ __forceinline__ void t8_setup(T8Ctx<K> &c, unsigned char *lds, const 
     c.rC = t8_rsrc(st.ch + (size_t)tile * g.n * kTile, (size_t)g.n * kTile * sizeof(double));
     c.eo8 = (uint32_t)c.f * 8u;
     c.lo8 = (uint32_t)(sub * kF8 + c.f) * 8u;
-    c.Tb = st.T + (size_t)blockIdx.x * g.max_row_deg * kF8 + c.f;
+    // rare-row scratch: one row per workgroup (two in the pair form: the T
+    // pool holds 2 x 8 x max_row_deg per tile, ldpc_api.cpp workspace)
+    c.Tb = st.T + ((size_t)blockIdx.x * (PAIR ? 2 : 1) + c.h) * g.max_row_deg * kF8 + c.f;
     c.S = (double *)(lds + ly.S) + c.f;
     c.LA = LA ? (double *)(lds + ly.LA) + c.f : nullptr;
     c.dummy = (double *)(lds + ly.dummy) + c.f;
@@ -681,12 +1045,12 @@ __device__ __forceinline__ void t8_syndrome(const DevGraph &g, const uint32_t *z
     if (acc) atomicOr((uint32_t *)bad + ff, 1u);
 }
 
-template <int K, bool LA, int D>
+template <int K, bool LA, int D, bool PAIR = false>
 __global__ __launch_bounds__(64 * kW8, 1) void tile8_kernel(DevGraph g, DevState st, int max_iter, int nllr,
                                                             const int *__restrict__ col_idx,
                                                             const int *__restrict__ row_ptr, AtanhCoef ac) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
-    const T8Layout ly = t8_layout(g.k, g.m, K, LA, D + 1);
+    const T8Layout ly = t8_layout(g.k, g.m, K, LA, PAIR ? 2 : D + 1);
     double *S = (double *)(lds + ly.S);
     double *LAl = LA ? (double *)(lds + ly.LA) : nullptr;
     uint32_t *zb = (uint32_t *)(lds + ly.zb);
@@ -723,12 +1087,12 @@ __global__ __launch_bounds__(64 * kW8, 1) void tile8_kernel(DevGraph g, DevState
     }
 
     T8Ctx<K> c;
-    t8_setup<K, LA>(c, lds, ly, g, st, tile, sub, col_idx, row_ptr, ac);
-    c.R = D + 1;
+    t8_setup<K, LA, PAIR>(c, lds, ly, g, st, tile, sub, col_idx, row_ptr, ac);
+    c.R = PAIR ? 2 : D + 1;
     // the identity edge's wavefront: with D = 3 wavefront 0, which otherwise
     // waits longest for the chain; with D = 2 the last one (wavefront 0's
     // body would bound the row period)
-    c.idwave = D >= 3 ? 0 : kW8 - 1;
+    c.idwave = D >= 3 && !PAIR ? 0 : kW8 - 1;
     const int fr = tile * kTile + sub * kF8 + c.f;  // this lane's frame
 
     for (int it = 0; it < max_iter; ++it) {
@@ -736,7 +1100,10 @@ __global__ __launch_bounds__(64 * kW8, 1) void tile8_kernel(DevGraph g, DevState
         c.live = livel[c.f] != 0;
         c.ep0 = t8_epoch0(it, g.m);
         T8_STAMP(w0);
-        t8_rows<K, LA, D>(c);
+        if constexpr (PAIR)
+            tp_rows<K>(c);
+        else
+            t8_rows<K, LA, D>(c);
         T8_STAMP(w1);
         T8_ADD(c, 8, w0, w1);
         __syncthreads();  // every P3 done: S complete, identity bits set
@@ -804,7 +1171,7 @@ __global__ __launch_bounds__(64 * kW8, 1) void tile8_kernel(DevGraph g, DevState
 // fresh; E in 8-frame blocks, L, ch and u bits in place) for the
 // column-parallel tail (ldpc_api.cpp mc_stream_point).  Reference: the
 // per-frame loop of main.py:295-342 over spa_decoder.py:63-280.
-template <int K, bool LA, int D>
+template <int K, bool LA, int D, bool PAIR = false>
 __global__ __launch_bounds__(64 * kW8, 1) void tile8_stream_kernel(
     DevGraph g, DevState st, int max_iter, int nllr, const int *__restrict__ col_idx,
     const int *__restrict__ row_ptr, AtanhCoef ac, uint64_t seed, int snr_point, double sigma, int64_t frame0,
@@ -812,7 +1179,7 @@ __global__ __launch_bounds__(64 * kW8, 1) void tile8_stream_kernel(
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     __shared__ long long gidx[kF8];  // refill: slot f's new frame index (< 0: none)
     __shared__ int nref;             // refill: some slot took a frame this pass
-    const T8Layout ly = t8_layout(g.k, g.m, K, LA, D + 1);
+    const T8Layout ly = t8_layout(g.k, g.m, K, LA, PAIR ? 2 : D + 1);
     double *S = (double *)(lds + ly.S);
     double *LAl = LA ? (double *)(lds + ly.LA) : nullptr;
     uint32_t *zb = (uint32_t *)(lds + ly.zb);
@@ -841,9 +1208,9 @@ __global__ __launch_bounds__(64 * kW8, 1) void tile8_stream_kernel(
     const __amdgpu_buffer_rsrc_t rL = t8_rsrc(st.L + (size_t)tile * g.n * kTile, (size_t)g.n * kTile * sizeof(double));
 
     T8Ctx<K> c;
-    t8_setup<K, LA>(c, lds, ly, g, st, tile, sub, col_idx, row_ptr, ac);
-    c.R = D + 1;
-    c.idwave = D >= 3 ? 0 : kW8 - 1;  // as tile8_kernel
+    t8_setup<K, LA, PAIR>(c, lds, ly, g, st, tile, sub, col_idx, row_ptr, ac);
+    c.R = PAIR ? 2 : D + 1;
+    c.idwave = D >= 3 && !PAIR ? 0 : kW8 - 1;  // as tile8_kernel
     const int m = g.m;
     const uint32_t *Ut = st.ubits + (size_t)tile * kw * kTile + sub * kF8 + lane;  // slot lanes only
 
@@ -907,7 +1274,10 @@ __global__ __launch_bounds__(64 * kW8, 1) void tile8_stream_kernel(
         c.fresh = freshl[c.f] != 0;
         c.first = false;
         c.ep0 = t8_epoch0(pass, m);
-        t8_rows<K, LA, D>(c);
+        if constexpr (PAIR)
+            tp_rows<K>(c);
+        else
+            t8_rows<K, LA, D>(c);
         __syncthreads();  // every P3 done: S complete, identity bits set
         if (threadIdx.x < kW8) c.p3row[threadIdx.x] = 0;
         t8_vn<LA>(g, S, LAl, zb, cntl, livel, rL, rC, sub, false, true, freshl, nllr);
@@ -956,21 +1326,23 @@ __global__ __launch_bounds__(64 * kW8, 1) void tile8_stream_kernel(
     }
 }
 
-// Variants: (K, L_A in LDS, pipeline depth D).  wimax_2304_0.5: (5, yes, 3);
-// the r3/4 codes: (8, no, 2) -- 8 slots per lane leave no registers for a
-// third row of t.
+// Variants: (K, L_A in LDS, pipeline depth D, pair form).  wimax_2304_0.5:
+// (5, yes, 3) or the pair form (10, yes, 2 pairs in flight); the r3/4 codes:
+// (8, no, 2) -- 8 slots per lane leave no registers for a third row of t.
 constexpr int kD5 = 3, kD8 = 2;
-template <int K, bool LA, int D>
+template <int K, bool LA, int D, bool PAIR = false>
 size_t t8_lds_bytes_k(const DevGraph &g) {
     if (!g.std_form || !g.a_packed || g.k <= 0 || g.n > 65535) return 0;
     const int C = (g.max_row_deg + kW8 - 1) / kW8;
-    if ((C + kQ8 - 1) / kQ8 > K) return 0;
-    const size_t b = t8_layout(g.k, g.m, K, LA, D + 1).total;
+    if ((C + (PAIR ? kPQ : kQ8) - 1) / (PAIR ? kPQ : kQ8) > K) return 0;
+    const size_t b = t8_layout(g.k, g.m, K, LA, PAIR ? 2 : D + 1).total;
     return b + 16 <= kLds8Max ? b : 0;  // + the static __shared__ counter(s)
 }
 
-// the variant a graph runs: 0 = none, else K * 2 + LA
+// the variant a graph runs: 0 = none, else K * 2 + LA (+ 100: the pair form,
+// DevGraph::t8pair, chosen at graph creation)
 int t8_variant(const DevGraph &g) {
+    if (g.t8pair && t8_lds_bytes_k<10, true, 2, true>(g)) return 100 + 10 * 2 + 1;
     if (t8_lds_bytes_k<5, true, kD5>(g)) return 5 * 2 + 1;
     if (t8_lds_bytes_k<8, false, kD8>(g)) return 8 * 2;
     return 0;
@@ -992,8 +1364,15 @@ bool tile8_applies(const DevGraph &g) {
     return mode == 1 || sub_frames(g) != 16;
 }
 
+bool tile8_pair_fits(const DevGraph &g) { return t8_lds_bytes_k<10, true, 2, true>(g) > 0; }
+
+// rare-row scratch rows per tile of the 8-frame decoder (ldpc_api.cpp sizes
+// the T pool: slots >= this x tiles)
+int tile8_scratch_per_tile(const DevGraph &g) { return t8_variant(g) >= 100 ? 2 : 1; }
+
 size_t tile8_lds_bytes(const DevGraph &g) {
     switch (t8_variant(g)) {
+        case 121: return t8_lds_bytes_k<10, true, 2, true>(g);
         case 11: return t8_lds_bytes_k<5, true, kD5>(g);
         case 16: return t8_lds_bytes_k<8, false, kD8>(g);
         default: return 0;
@@ -1010,10 +1389,16 @@ hipError_t launch_tile8_stream(const DevGraph &g, const DevState &st, int max_it
                                int snr_point, double sigma, int64_t frame0, int64_t total, unsigned long long *next,
                                unsigned long long *ctr, int64_t handoff, hipStream_t s) {
     const size_t lds = tile8_lds_bytes(g);
-    if (!tile8_stream_lds_bytes(g) || g.ef != kF8 || !g.a_packed || !st.ubits || st.ntiles > st.nslots)
+    if (!tile8_stream_lds_bytes(g) || g.ef != kF8 || !g.a_packed || !st.ubits ||
+        st.ntiles * tile8_scratch_per_tile(g) > st.nslots)
         return hipErrorInvalidValue;
     const dim3 grid(st.ntiles * kQ8), block(64 * kW8);
     switch (t8_variant(g)) {
+        case 121:
+            tile8_stream_kernel<10, true, 2, true><<<grid, block, lds, s>>>(g, st, max_iter, nllr ? 1 : 0, g.col_idx,
+                                                                         g.row_ptr, kAtanhCoef, seed, snr_point,
+                                                                         sigma, frame0, total, next, ctr, handoff);
+            break;
         case 11:
             tile8_stream_kernel<5, true, kD5><<<grid, block, lds, s>>>(g, st, max_iter, nllr ? 1 : 0, g.col_idx,
                                                                       g.row_ptr, kAtanhCoef, seed, snr_point, sigma,
@@ -1032,9 +1417,13 @@ hipError_t launch_tile8_stream(const DevGraph &g, const DevState &st, int max_it
 
 hipError_t launch_tile8(const DevGraph &g, const DevState &st, int max_iter, bool nllr, hipStream_t s) {
     const size_t lds = tile8_lds_bytes(g);
-    if (!lds || g.ef != kF8 || st.ntiles > st.nslots) return hipErrorInvalidValue;
+    if (!lds || g.ef != kF8 || st.ntiles * tile8_scratch_per_tile(g) > st.nslots) return hipErrorInvalidValue;
     const dim3 grid(st.ntiles * kQ8), block(64 * kW8);
     switch (t8_variant(g)) {
+        case 121:
+            tile8_kernel<10, true, 2, true><<<grid, block, lds, s>>>(g, st, max_iter, nllr ? 1 : 0, g.col_idx,
+                                                                  g.row_ptr, kAtanhCoef);
+            break;
         case 11:
             tile8_kernel<5, true, kD5><<<grid, block, lds, s>>>(g, st, max_iter, nllr ? 1 : 0, g.col_idx, g.row_ptr,
                                                                kAtanhCoef);

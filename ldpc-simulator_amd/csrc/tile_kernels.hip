@@ -691,7 +691,7 @@ size_t tile_lds_bytes(const DevGraph &g) {
 
 const char *tile_kernel_name(const DevGraph &g) {
     if (tile64_lds_bytes(g)) return "tile_kernel";
-    if (g.ef == 8) return tile8_lds_bytes(g) ? "tile8_kernel" : "";
+    if (g.ef == 8) return tile8_lds_bytes(g) ? (tile8_scratch_per_tile(g) == 2 ? "tile8_kernel:pair" : "tile8_kernel") : "";
     if (sub_enabled(g) && sub_lds_bytes(g)) return "tile_sub_kernel";
     return "";
 }

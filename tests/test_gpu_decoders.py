@@ -52,8 +52,8 @@ def _routes_for(code):
     out = [("edge", None), ("split", None), ("tile", None)]
     if code in LONG:
         out.append(("cols", None))
-    if code == "wimax_2304_0.5":  # the headline code also through tile8 and its 8-frame split path
-        out += [("tile", 8), ("split", 8)]
+    if code == "wimax_2304_0.5":  # the headline code also through tile8 (row and pair form) and its 8-frame split path
+        out += [("tile", 8), ("split", 8), ("tile", "8p")]
     if code in ("wimax_2304_0.75A", "wimax_2304_0.75B"):  # the r3/4 codes in the 64-frame layout
         out += [("split", 64), ("cols", 64)]
     return out
@@ -62,9 +62,9 @@ def _routes_for(code):
 def _tile_name(code, layout):
     if code in ("BCH_7_4_1_strip", "wimax_576_0.5"):
         return "tile_kernel"
-    if code == "wimax_2304_0.5" and layout != 8:
+    if code == "wimax_2304_0.5" and layout not in (8, "8p"):
         return "tile_sub_kernel"
-    return "tile8_kernel"
+    return "tile8_kernel:pair" if layout == "8p" else "tile8_kernel"
 
 
 _GRAPHS = {}
@@ -75,12 +75,16 @@ def _graph(code, layout, monkeypatch):
     key = (code, layout)
     if key not in _GRAPHS:
         if layout is not None:
-            monkeypatch.setenv("LDPC_TILE8", "1" if layout == 8 else "0")
+            monkeypatch.setenv("LDPC_TILE8", "0" if layout == 64 else "1")
+        if layout == "8p":
+            monkeypatch.setenv("LDPC_T8_PAIR", "1")
         try:
             _GRAPHS[key] = Graph(hstd_for(code))
         finally:
             if layout is not None:
                 monkeypatch.delenv("LDPC_TILE8")
+            if layout == "8p":
+                monkeypatch.delenv("LDPC_T8_PAIR")
     return _GRAPHS[key]
 
 
@@ -171,6 +175,56 @@ def test_tile8_matches_oracle_config4_sweep(gpu_available, monkeypatch, code, sn
         assert_llr_close(r.msgs, o["msgs"], "messages E", slack=sl_E)
     if snr == 4.0 and code.endswith("A"):
         assert (r.status == 1).mean() > 0.9  # the reference's own cliff (golden w2304A_T3_4dB)
+
+
+_PAIR = [(s, n) for s in (1.0, 2.0, 3.0) for n in (72,)] + [(2.0, 130)]
+
+
+@pytest.mark.parametrize("snr,B", _PAIR, ids=[f"{s}dB-{n}" for s, n in _PAIR])
+def test_tile8_pair_matches_oracle(gpu_available, monkeypatch, snr, B):
+    """tile8's pair form (two rows per wavefront, wimax_2304_0.5) vs the oracle
+    at T=50: 72 frames (one full tile + one live 8-frame sub-tile) and 130
+    (two full tiles + a 2-frame sub-tile)."""
+    code = "wimax_2304_0.5"
+    H = hstd_for(code)
+    T = 50
+    llr = _random_llr(H, B, snr, seed=5100 + int(10 * snr) + B)
+    r = _run_route(code, "8p", "tile", llr, T, monkeypatch, nllr=True, post=True, msgs=True)
+    o = oracle.spa_decode(H, llr, T, nllr=True, want_E=True)
+    for key in ("z", "conv", "status", "iters", "nllr"):
+        np.testing.assert_array_equal(r[key], o[key], err_msg=key)
+    try:
+        assert_llr_close(r.post, o["post"], "posterior L")
+        assert_llr_close(r.msgs, o["msgs"], "messages E")
+    except AssertionError:
+        sl_L, sl_E = oracle.conditioning_slack(H, llr, T, nllr=True)
+        assert_llr_close(r.post, o["post"], "posterior L", slack=sl_L)
+        assert_llr_close(r.msgs, o["msgs"], "messages E", slack=sl_E)
+
+
+def test_tile8_pair_rare_rows(gpu_available, monkeypatch):
+    """The pair form's rare path (|t| <= 1e-10: the product of the others,
+    spa_decoder.py:159-164): frames with exact-zero channel LLRs on some
+    columns (rows with one zero t in either half of a pair, rows with two),
+    vs the oracle, T = 5."""
+    code = "wimax_2304_0.5"
+    H = hstd_for(code)
+    B, T = 24, 5
+    llr = _random_llr(H, B, 2.0, seed=77)
+    rng = np.random.default_rng(78)
+    for f in range(B):
+        llr[f, rng.choice(H.shape[1], size=1 + f % 4, replace=False)] = 0.0
+    r = _run_route(code, "8p", "tile", llr, T, monkeypatch, nllr=True, post=True, msgs=True)
+    o = oracle.spa_decode(H, llr, T, nllr=True, want_E=True)
+    for key in ("z", "conv", "status", "iters", "nllr"):
+        np.testing.assert_array_equal(r[key], o[key], err_msg=key)
+    try:
+        assert_llr_close(r.post, o["post"], "posterior L")
+        assert_llr_close(r.msgs, o["msgs"], "messages E")
+    except AssertionError:
+        sl_L, sl_E = oracle.conditioning_slack(H, llr, T, nllr=True)
+        assert_llr_close(r.post, o["post"], "posterior L", slack=sl_L)
+        assert_llr_close(r.msgs, o["msgs"], "messages E", slack=sl_E)
 
 
 def test_cutover_thresholds(gpu_available, monkeypatch):

@@ -243,6 +243,9 @@ def test_tile8_stream_matches_oracle_config4(gpu_available):
     p = dec.profile_read()
     dec.profile(False)
     assert p["tile"][1] == len(snrs), p  # one tile8_stream_kernel launch per point
+    # ... which handed its last running frames to the split path's tail
+    # (cn_sub_kernel stream form + vn_cols_kernel + tail_exit_kernel)
+    assert p["cn"][1] > 0 and p["vn_cols"][1] > 0, p
     gen = _decoder(code, frames)
     for i, sg in enumerate(sig):
         u, llr = gen.generate(SEED, i, sg, 5000, frames)
@@ -250,6 +253,32 @@ def test_tile8_stream_matches_oracle_config4(gpu_available):
         want = oracle.main_counters(u, o["z"], o["status"], o["conv"],
                                     nllr_cnt=np.rint(o["nllr"] * k).astype(np.int64), iters=o["iters"])
         np.testing.assert_array_equal(ctr[i], want, err_msg=f"{snrs[i]} dB")
+
+
+@pytest.mark.parametrize("snr", [2.5, 3.0])
+def test_sub_stream_handoff_matches_oracle(gpu_available, snr):
+    """The headline code's streaming path end to end against the oracle:
+    tile_sub_stream_kernel (16-frame sub-tiles) -> hand-off at supply end ->
+    the split tail (cn_sub_kernel's stream form + vn_cols_kernel +
+    tail_exit_kernel), 192 frames through 64 slots at T = 50, so the tail
+    carries frames that started in the stream kernel; counters == the
+    oracle's main.py counters on the very frames the device generated."""
+    code, cap, frames, T = "wimax_2304_0.5", 64, 192, 50
+    H = hstd_for(code)
+    k = H.shape[1] - H.shape[0]
+    sg = oracle.sigma_for_snr(snr)
+    dec = _decoder(code, cap)
+    dec.profile(True)
+    ctr = dec.mc_run(SEED, [sg], frames, 7000, T, nllr=True)
+    p = dec.profile_read()
+    dec.profile(False)
+    assert p["tile"][1] == 1, p  # one tile_sub_stream_kernel launch
+    assert p["cn"][1] > 0 and p["vn_cols"][1] > 0, p  # the split tail ran
+    u, llr = _decoder(code, frames).generate(SEED, 0, sg, 7000, frames)
+    o = oracle.spa_decode(H, llr, T, nllr=True)
+    want = oracle.main_counters(u, o["z"], o["status"], o["conv"],
+                                nllr_cnt=np.rint(o["nllr"] * k).astype(np.int64), iters=o["iters"])
+    np.testing.assert_array_equal(ctr[0], want)
 
 
 def test_tile8_stream_r12_equals_static(gpu_available, monkeypatch):
