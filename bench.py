@@ -111,6 +111,9 @@ def parse():
                     help="parity mode: BASELINE config 5 (DVB-S2 n=64800 r1/2 profile, physical mode only: its "
                          "H_std would have ~5e8 edges) under 'config5' (0 = none)")
     ap.add_argument("--config5-frames", type=int, default=8192, help="config-5 frames per GPU per step")
+    ap.add_argument("--config5-waterfall-snr", type=float, default=-2.5,
+                    help="a second config-5 point in the waterfall, where the 50-iteration decoder iterates "
+                         "(~30 average iterations at -2.5 dB; NaN = none)")
     ap.add_argument("--dropin-calls", type=int, default=20,
                     help="parity mode: one-frame decode() calls timed under 'dropin' (main.py's call pattern; 0 = none)")
     ap.add_argument("--stub", action="store_true",
@@ -265,10 +268,11 @@ def profile_order(d):
     return (int(mt.group(1)), len(mt.group(2)), mt.group(2), d) if mt else (-1, 0, "", d)
 
 
-def committed_traffic(nnz, frames, kernel="cn"):
+def committed_traffic(nnz, frames, kernel="cn", snr=None):
     """HBM bytes per cn_kernel launch from the newest committed PMC pass
     (profiles/*/traffic.json, tools/profile.sh + tools/summarize_profile.py)
-    for this exact workload shape, or (None, None)."""
+    for this exact workload shape (and SNR, where the file records one and
+    `snr` is given), or (None, None)."""
     pdir = os.path.join(ROOT, "profiles")
     best = None
     for d in sorted(os.listdir(pdir), key=profile_order) if os.path.isdir(pdir) else []:
@@ -279,6 +283,8 @@ def committed_traffic(nnz, frames, kernel="cn"):
                 continue
             f = os.path.join(pdir, d, fn)
             t = json.load(open(f))
+            if snr is not None and "snr_db" in t and abs(float(t["snr_db"]) - snr) > 1e-9:
+                continue
             if t.get("edges") == nnz and t.get("frames") == frames:
                 k = t.get("kernels", {})
                 cn = k.get(kernel) or (k.get("cn_kernel<false>") if kernel == "cn" else None)
@@ -605,7 +611,11 @@ def config5_extra(args, local, world, rank, dist):
     structure and degree profile with a SEEDED address table (the ETSI table
     is not available offline: ldpc_amd/ira.py), so this is a stress test of
     the long irregular code's decoder, with no parity to the reference.  State
-    in HBM (phys_cn_tile / phys_vn_tile), on-device IRA encoder."""
+    in HBM (phys_cn_tile / phys_vn_tile), on-device IRA encoder.  Two points:
+    the headline's SNR (1 dB on the reference axis: ~2 iterations) and the
+    waterfall (--config5-waterfall-snr, -2.5 dB: ~30 of the 50 iterations,
+    the long-block stress BASELINE names), each with the CN kernel's roofline
+    and its committed PMC traffic (tools/profile_phys.sh on config 5)."""
     from ldpc_amd import ira
     from ldpc_amd.device import Decoder, Graph
     H = ira.dvbs2_profile_matrix()
@@ -614,41 +624,51 @@ def config5_extra(args, local, world, rank, dist):
     g = Graph(H, device=local)
     F = args.config5_frames
     dec = Decoder(g, F)
-    sig = 1.0 / math.sqrt(2.0 * (10.0 ** (args.snr * 0.1)))
-    base = 1 << 45
-    dec.phys_mc_run(g, SEED, [sig], F, base - F, args.iters)  # warm-up
-    barrier(dist, local)
-    dec.profile_read()
-    dec.profile(True)
-    t1 = time.perf_counter()
-    loc = np.zeros((1, 7), np.int64)
-    tot = np.zeros((1, 7), np.int64)
-    steps = 2
-    for st in range(steps):
-        c = dec.phys_mc_run(g, SEED, [sig], F, base + (st * world + rank) * F, args.iters)
-        loc += c
-        tot += allreduce_counters(dist, c, local)
-    barrier(dist, local)
-    dt = max_over_ranks(dist, time.perf_counter() - t1, local)
-    dec.profile(False)
-    prof = dec.profile_read()
-    dec.close()
-    cms, cl = prof["phys_cn"]
-    f = int(tot[0, 0])
+
+    def point(snr, base):
+        sig = 1.0 / math.sqrt(2.0 * (10.0 ** (snr * 0.1)))
+        dec.phys_mc_run(g, SEED, [sig], F, base - F, args.iters)  # warm-up
+        barrier(dist, local)
+        dec.profile_read()
+        dec.profile(True)
+        t1 = time.perf_counter()
+        loc = np.zeros((1, 7), np.int64)
+        tot = np.zeros((1, 7), np.int64)
+        steps = 2
+        for st in range(steps):
+            c = dec.phys_mc_run(g, SEED, [sig], F, base + (st * world + rank) * F, args.iters)
+            loc += c
+            tot += allreduce_counters(dist, c, local)
+        barrier(dist, local)
+        dt = max_over_ranks(dist, time.perf_counter() - t1, local)
+        dec.profile(False)
+        prof = dec.profile_read()
+        cms, cl = prof["phys_cn"]
+        f = int(tot[0, 0])
+        out = {"snr_db": snr, "max_iter": args.iters, "frames_per_gpu_step": F, "steps": steps, "n_gpus": world,
+               "value": f / dt, "unit": "codewords/s", "info_bits_per_s": f * k / dt,
+               "ms_per_step": dt / steps * 1e3, "avg_iters": int(tot[0, 6]) / max(f, 1),
+               "fer": int(tot[0, 1]) / max(f, 1), "dtype": "f32"}
+        if cl:
+            cn_bytes = 12.0 * H.nnz * int(loc[0, 6])
+            tr, tsrc = committed_traffic(int(H.nnz), F, "phys_cn", snr)
+            out["roofline"] = {"bound": "hbm", "kernel": "phys_cn_tile_kernel", "launches": cl,
+                               "achieved": cn_bytes / (cms / 1e3) / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                               "frac": cn_bytes / (cms / 1e3) / 1e9 / HBM_PEAK_GBS,
+                               "traffic": tr, "traffic_source": tsrc, "bytes_per_launch": cn_bytes / cl,
+                               "bytes_model": "12 B x H edges x frame-iterations (L[col] gather + E_old read + "
+                                              "E_new write, fp32), over the CN launches' HIP-event time; traffic = "
+                                              "committed PMC bytes per CN launch at this SNR (compare "
+                                              "bytes_per_launch)"}
+        return out
+
     out = {"what": "BASELINE config 5: DVB-S2 n=64800 r1/2 profile (seeded address table), physical mode "
                    "(fp32, sparse graph, state in HBM) -- no reference parity",
-           "code": "dvbs2_profile_64800_0.5", "n": n, "k": k, "edges_H": int(H.nnz), "snr_db": args.snr,
-           "max_iter": args.iters, "frames_per_gpu_step": F, "steps": steps, "n_gpus": world,
-           "value": f / dt, "unit": "codewords/s", "info_bits_per_s": f * k / dt,
-           "ms_per_step": dt / steps * 1e3, "avg_iters": int(tot[0, 6]) / max(f, 1),
-           "fer": int(tot[0, 1]) / max(f, 1), "dtype": "f32"}
-    if cl:
-        cn_bytes = 12.0 * H.nnz * int(loc[0, 6])
-        out["roofline"] = {"bound": "hbm", "kernel": "phys_cn_tile_kernel", "launches": cl,
-                           "achieved": cn_bytes / (cms / 1e3) / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                           "frac": cn_bytes / (cms / 1e3) / 1e9 / HBM_PEAK_GBS,
-                           "bytes_model": "12 B x H edges x frame-iterations (L[col] gather + E_old read + "
-                                          "E_new write, fp32), over the CN launches' HIP-event time"}
+           "code": "dvbs2_profile_64800_0.5", "n": n, "k": k, "edges_H": int(H.nnz)}
+    out.update(point(args.snr, 1 << 45))
+    if not math.isnan(args.config5_waterfall_snr):
+        out["waterfall"] = point(args.config5_waterfall_snr, (1 << 45) + (1 << 40))
+    dec.close()
     return out
 
 

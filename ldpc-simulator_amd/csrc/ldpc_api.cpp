@@ -95,6 +95,11 @@ struct ldpc_decoder {
 
 namespace {
 
+// scratch slots (max_row_deg x 64 doubles) per tile the tile decoders need:
+// two buffers of a row per workgroup (rare rows alternate), four for tile8's
+// pair form (two rows per wavefront)
+int tile_scratch_rows(const DevGraph &g) { return g.ef == 8 ? ldpc::tile8_scratch_per_tile(g) : 2; }
+
 // Sub-tile decoder's S order (tile_sub.hip sub_p3): wavefront w's P3 of row r
 // waits for row r-1's P3 by wavefronts [lo, hi], those whose chunk's extended
 // column span (from just past the previous non-empty chunk's last column to
@@ -346,7 +351,7 @@ int run_iterations(ldpc_decoder *d, const DevGraph &G, const DevState &st_in, in
         return e == hipSuccess ? LDPC_OK
                                : ldpc_fail(LDPC_EDEVICE, "decode iterations: %s", hipGetErrorString(e));
     };
-    if (!split && !cols && ldpc::use_tile(G) && st.ntiles <= st.nslots)  // one launch: every tile to its own exit
+    if (!split && !cols && ldpc::use_tile(G) && st.ntiles * tile_scratch_rows(G) <= st.nslots)  // one launch: every tile to its own exit
         return hip(timed(d, LDPC_K_TILE, s, [&] { return ldpc::launch_tile(G, st, max_iter, nllr, s); }));
     // cn_rare_kernel clears the OTHER parity's count for the next CN; the one
     // the last iteration used (or an early stop left) is cleared here
@@ -395,8 +400,7 @@ int run_iterations(ldpc_decoder *d, const DevGraph &G, const DevState &st_in, in
 
 // cn_rare_kernel runs 1024 blocks x 4 wavefronts; one scratch slot each.
 int scratch_slots() { return 4096; }
-// scratch slots (max_row_deg x 64 doubles) per tile the tile decoders need
-int tile_scratch_rows(const DevGraph &g) { return g.ef == 8 ? ldpc::tile8_scratch_per_tile(g) : 1; }
+
 
 size_t workspace_bytes(const DevGraph &g, int cap_tiles) {
     const size_t cap = (size_t)cap_tiles * kTile;
@@ -977,7 +981,7 @@ int mc_stream_point(ldpc_decoder *d, uint64_t seed, int p, double sigma, int64_t
                      [&] { return ldpc::launch_refill(G, st, seed, p, sigma, frame0, total, next, s); });
     };
     int cur = ntiles;  // tiles the steps launch (shrinks as the tail is compacted)
-    if (!split && ldpc::use_tile_stream(G) && st.ntiles <= st.nslots) {
+    if (!split && ldpc::use_tile_stream(G) && st.ntiles * tile_scratch_rows(G) <= st.nslots) {
         // one launch: every workgroup's lanes pull frames until the supply is
         // out; the sub-tile decoder hands its last running frames to the
         // column-parallel tail below (one pass of a sub-tile costs ~14 ms)

@@ -157,7 +157,8 @@ struct T8Ctx {
     __amdgpu_buffer_rsrc_t rE;  // this workgroup's E block: edge e, frame f at e*64 + f*8
     __amdgpu_buffer_rsrc_t rL, rC;  // the tile's L / ch: column c at c*512 + lo8
     uint32_t eo8, lo8;
-    double *Tb;      // rare-row scratch of this workgroup, position p at [p * 8]
+    double *Tb;      // rare-row scratch of this workgroup, position p at [p * 8]; two buffers
+    size_t tbuf;     // doubles between them (rare rows alternate: tile_kernels.hip)
     double *S;       // LDS, column c at [c * 8] (this lane's frame added)
     double *LA;      // LDS, same indexing (null: L gathered from global)
     double *dummy;   // LDS, this lane's frame
@@ -466,12 +467,13 @@ __device__ __forceinline__ void t8_p3(T8Ctx<K> &c, int r, double (&t)[K]) {
         // :164) for an edge with |t| <= 1e-10; t parked at row positions (the
         // identity edge at deg-1).  Every wavefront takes part in the count.
         const int pos0 = rc.c0 + c.j * rc.CS - rc.beg;
+        double *tb = c.Tb + (c.ntiny & 1) * c.tbuf;  // the next rare row parks in the other buffer
         if (rc.cnt > 0) {
 #pragma unroll
             for (int i = 0; i < K; ++i)
-                if (i < nj) c.Tb[(size_t)(pos0 + i) * kF8] = t[i];
+                if (i < nj) tb[(size_t)(pos0 + i) * kF8] = t[i];
         }
-        if (idw && c.j == 0) c.Tb[(size_t)(rc.deg - 1) * kF8] = tI;
+        if (idw && c.j == 0) tb[(size_t)(rc.deg - 1) * kF8] = tI;
         __builtin_amdgcn_s_waitcnt(0);  // scratch stores have reached L2
         c.ntiny += 1;
         if ((threadIdx.x & 63) == 0) __hip_atomic_fetch_add(c.tseq, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -481,7 +483,7 @@ __device__ __forceinline__ void t8_p3(T8Ctx<K> &c, int r, double (&t)[K]) {
             bool fst = true;
             for (int p = 0; p < rc.deg; ++p) {
                 if (p == pos) continue;
-                const double t2 = ld_l2(c.Tb + (size_t)p * kF8);
+                const double t2 = ld_l2(tb + (size_t)p * kF8);
                 q = fst ? t2 : q * t2;
                 fst = false;
             }
@@ -868,11 +870,12 @@ __device__ __forceinline__ void tp_p3(T8Ctx<K> &c, int q, double (&t)[K], TpStag
         // :164) for an edge with |t| <= 1e-10 of a tiny row; t parked at row
         // positions (the identity edge at deg-1), every wavefront counts
         const int pos0 = rc.c0 + c.j * rc.CS - rc.beg;
+        double *tb = c.Tb + (c.ntiny & 1) * c.tbuf;  // the next rare pair parks in the other buffer
         if (tiny_row) {
 #pragma unroll
             for (int i = 0; i < K; ++i)
-                if (i < nj) c.Tb[(size_t)(pos0 + i) * kF8] = t[i];
-            if (idw && c.j == 0) c.Tb[(size_t)(rc.deg - 1) * kF8] = tI;
+                if (i < nj) tb[(size_t)(pos0 + i) * kF8] = t[i];
+            if (idw && c.j == 0) tb[(size_t)(rc.deg - 1) * kF8] = tI;
         }
         __builtin_amdgcn_s_waitcnt(0);  // scratch stores have reached L2
         c.ntiny += 1;
@@ -883,7 +886,7 @@ __device__ __forceinline__ void tp_p3(T8Ctx<K> &c, int q, double (&t)[K], TpStag
             bool fst = true;
             for (int p = 0; p < rc.deg; ++p) {
                 if (p == pos) continue;
-                const double t2 = ld_l2(c.Tb + (size_t)p * kF8);
+                const double t2 = ld_l2(tb + (size_t)p * kF8);
                 qq = fst ? t2 : qq * t2;
                 fst = false;
             }
@@ -963,9 +966,11 @@ __device__ __forceinline__ void t8_setup(T8Ctx<K> &c, unsigned char *lds, const 
     c.rC = t8_rsrc(st.ch + (size_t)tile * g.n * kTile, (size_t)g.n * kTile * sizeof(double));
     c.eo8 = (uint32_t)c.f * 8u;
     c.lo8 = (uint32_t)(sub * kF8 + c.f) * 8u;
-    // rare-row scratch: one row per workgroup (two in the pair form: the T
-    // pool holds 2 x 8 x max_row_deg per tile, ldpc_api.cpp workspace)
-    c.Tb = st.T + ((size_t)blockIdx.x * (PAIR ? 2 : 1) + c.h) * g.max_row_deg * kF8 + c.f;
+    // rare-row scratch: two buffers of one row per workgroup (of two rows in
+    // the pair form: the T pool holds 4 x 8 x 2 x max_row_deg per tile,
+    // ldpc_api.cpp workspace)
+    c.Tb = st.T + ((size_t)blockIdx.x * (PAIR ? 2 : 1) + c.h) * 2 * g.max_row_deg * kF8 + c.f;
+    c.tbuf = (size_t)g.max_row_deg * kF8;
     c.S = (double *)(lds + ly.S) + c.f;
     c.LA = LA ? (double *)(lds + ly.LA) + c.f : nullptr;
     c.dummy = (double *)(lds + ly.dummy) + c.f;
@@ -1368,7 +1373,7 @@ bool tile8_pair_fits(const DevGraph &g) { return t8_lds_bytes_k<10, true, 2, tru
 
 // rare-row scratch rows per tile of the 8-frame decoder (ldpc_api.cpp sizes
 // the T pool: slots >= this x tiles)
-int tile8_scratch_per_tile(const DevGraph &g) { return t8_variant(g) >= 100 ? 2 : 1; }
+int tile8_scratch_per_tile(const DevGraph &g) { return t8_variant(g) >= 100 ? 4 : 2; }
 
 size_t tile8_lds_bytes(const DevGraph &g) {
     switch (t8_variant(g)) {

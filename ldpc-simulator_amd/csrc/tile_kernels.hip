@@ -125,7 +125,8 @@ struct TileCtx {
     double *Eb;        // messages E
     double *Lb;        // posteriors
     const double *Cb;  // channel LLRs
-    double *Tb;        // rare-row scratch slot of this workgroup
+    double *Tb;        // rare-row scratch slot of this workgroup: two buffers, by rare-row parity
+    size_t tbuf;       // doubles between the two buffers
     double *S;         // LDS [k][64]
     double *slot;      // LDS [kTR][64]
     uint32_t *ib;      // LDS [mw][64] z^1 of the identity columns
@@ -238,10 +239,14 @@ __device__ __forceinline__ void tile_p3(TileCtx &c, int r, double (&t)[kTK]) {
             if (i < rc.cnt) t[i] = 2.0 * atanh_f(clip_cl(P / t[i]), c.ltab, c.ac);  // :159-168
     } else {
         // rare: q = prod of the others, in order (np.prod(np.delete(...)), :164)
+        // the rare rows alternate between two scratch buffers: a wavefront
+        // parks the next rare row's t only after every wavefront has counted
+        // that row, i.e. finished reading this one
+        double *tb = c.Tb + (c.ntiny & 1) * c.tbuf;
         const int pos0 = c.wave * rc.C;
 #pragma unroll
         for (int i = 0; i < kTK; ++i)
-            if (i < rc.cnt) *at(c.Tb, pos0 + i, c.lane) = t[i];
+            if (i < rc.cnt) *at(tb, pos0 + i, c.lane) = t[i];
         __builtin_amdgcn_s_waitcnt(0);  // scratch stores have reached L2
         c.ntiny += 1;
         if (c.lane == 0) __hip_atomic_fetch_add(c.tseq, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -258,7 +263,7 @@ __device__ __forceinline__ void tile_p3(TileCtx &c, int r, double (&t)[kTK]) {
                     bool fst = true;
                     for (int p = 0; p < rc.deg; ++p) {
                         if (p == pos0 + i) continue;
-                        const double t2 = ld_l2(at(c.Tb, p, c.lane));
+                        const double t2 = ld_l2(at(tb, p, c.lane));
                         q = fst ? t2 : q * t2;
                         fst = false;
                     }
@@ -403,7 +408,8 @@ __global__ __launch_bounds__(64 * kTW, 1) void tile_kernel(DevGraph g, DevState 
     c.Eb = st.E + (size_t)tile * g.nnz * kTile;
     c.Lb = st.L + (size_t)tile * g.n * kTile;
     c.Cb = st.ch + (size_t)tile * g.n * kTile;
-    c.Tb = st.T + (size_t)blockIdx.x * g.max_row_deg * kTile;
+    c.Tb = st.T + (size_t)blockIdx.x * 2 * g.max_row_deg * kTile;
+    c.tbuf = (size_t)g.max_row_deg * kTile;
     c.S = S;
     c.slot = (double *)(lds + ly.slot);
     c.ib = ib;
@@ -539,7 +545,8 @@ __global__ __launch_bounds__(64 * kTW, 1) void tile_stream_kernel(DevGraph g, De
     c.Eb = st.E + (size_t)tile * g.nnz * kTile;
     c.Lb = st.L + (size_t)tile * g.n * kTile;
     c.Cb = st.ch + (size_t)tile * g.n * kTile;
-    c.Tb = st.T + (size_t)blockIdx.x * g.max_row_deg * kTile;
+    c.Tb = st.T + (size_t)blockIdx.x * 2 * g.max_row_deg * kTile;
+    c.tbuf = (size_t)g.max_row_deg * kTile;
     c.S = S;
     c.slot = (double *)(lds + ly.slot);
     c.ib = ib;
@@ -691,7 +698,7 @@ size_t tile_lds_bytes(const DevGraph &g) {
 
 const char *tile_kernel_name(const DevGraph &g) {
     if (tile64_lds_bytes(g)) return "tile_kernel";
-    if (g.ef == 8) return tile8_lds_bytes(g) ? (tile8_scratch_per_tile(g) == 2 ? "tile8_kernel:pair" : "tile8_kernel") : "";
+    if (g.ef == 8) return tile8_lds_bytes(g) ? (g.t8pair ? "tile8_kernel:pair" : "tile8_kernel") : "";
     if (sub_enabled(g) && sub_lds_bytes(g)) return "tile_sub_kernel";
     return "";
 }
@@ -733,14 +740,14 @@ hipError_t launch_tile_stream(const DevGraph &g, const DevState &st, int max_ite
     if (!lds && sub16(g))
         return launch_tile_sub_stream(g, st, max_iter, nllr, seed, snr_point, sigma, frame0, total, next, ctr,
                                       handoff, s);
-    if (!lds || !g.a_packed || !st.ubits || st.ntiles > st.nslots) return hipErrorInvalidValue;
+    if (!lds || !g.a_packed || !st.ubits || 2 * st.ntiles > st.nslots) return hipErrorInvalidValue;
     tile_stream_kernel<<<st.ntiles, 64 * kTW, lds, s>>>(g, st, max_iter, nllr ? 1 : 0, g.col_idx, g.row_ptr,
                                                         kAtanhCoef, seed, snr_point, sigma, frame0, total, next, ctr);
     return hipGetLastError();
 }
 
 hipError_t launch_tile(const DevGraph &g, const DevState &st, int max_iter, bool nllr, hipStream_t s) {
-    if (st.ntiles > st.nslots) return hipErrorInvalidValue;
+    if (2 * st.ntiles > st.nslots) return hipErrorInvalidValue;  // two rare-row buffers per tile
     const size_t lds = tile64_lds_bytes(g);
     if (!lds && g.ef == 8) return launch_tile8(g, st, max_iter, nllr, s);
     if (!lds) return sub_enabled(g) ? launch_tile_sub(g, st, max_iter, nllr, s) : hipErrorInvalidValue;

@@ -154,7 +154,8 @@ struct SubCtx {
     double *Eb;
     double *Lb;
     const double *Cb;
-    double *Tb;     // rare-row scratch of this workgroup, element (pos) at [pos * F]
+    double *Tb;     // rare-row scratch of this workgroup, element (pos) at [pos * F]; two buffers
+    size_t tbuf;    // doubles between them (rare rows alternate: tile_kernels.hip)
     double *S;      // LDS, element (col) at [col * F]
     double *dummy;  // LDS, this lane's frame
     double *slot;   // LDS, chain slot s at [s * F]
@@ -455,9 +456,10 @@ __device__ __forceinline__ void sub_p3_body(SubCtx<Q> &c, int r, double (&t)[Sub
         // rare: q = in-order product of the others (np.prod(np.delete(...)),
         // :164) for an edge with |t| <= 1e-10; t parked at row positions
         const int rb = c.row_ptr[r];
+        double *tb = c.Tb + (c.ntiny & 1) * c.tbuf;  // the next rare row parks in the other buffer
 #pragma unroll
         for (int i = 0; i < K; ++i)
-            if (i < rc.CS && i < nj) c.Tb[(size_t)(sub_edge(c, rc, i) - rb) * F] = t[i];
+            if (i < rc.CS && i < nj) tb[(size_t)(sub_edge(c, rc, i) - rb) * F] = t[i];
         __builtin_amdgcn_s_waitcnt(0);  // scratch stores have reached L2
         c.ntiny += 1;
         if ((threadIdx.x & 63) == 0) __hip_atomic_fetch_add(c.tseq, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -475,7 +477,7 @@ __device__ __forceinline__ void sub_p3_body(SubCtx<Q> &c, int r, double (&t)[Sub
                     bool fst = true;
                     for (int p = 0; p < rc.deg; ++p) {
                         if (p == pos) continue;
-                        const double t2 = ld_l2(c.Tb + (size_t)p * F);
+                        const double t2 = ld_l2(tb + (size_t)p * F);
                         q = fst ? t2 : q * t2;
                         fst = false;
                     }
@@ -609,7 +611,8 @@ __global__ __launch_bounds__(64 * kSW, 1) void tile_sub_kernel(DevGraph g, DevSt
     c.Lu = (const char *)(st.L + (size_t)tile * g.n * kTile);
     c.Cu = (const char *)(st.ch + (size_t)tile * g.n * kTile);
     c.lo8 = (uint32_t)lo * 8u;
-    c.Tb = st.T + (size_t)blockIdx.x * g.max_row_deg * F + f;
+    c.Tb = st.T + (size_t)blockIdx.x * 2 * g.max_row_deg * F + f;
+    c.tbuf = (size_t)g.max_row_deg * F;
     c.S = S + f;
     c.dummy = (double *)(lds + ly.dummy) + f;
     c.slot = (double *)(lds + ly.slot) + f;
@@ -780,7 +783,8 @@ __global__ __launch_bounds__(64 * kSW, 1) void tile_sub_stream_kernel(
     c.Lu = (const char *)(st.L + (size_t)tile * g.n * kTile);
     c.Cu = (const char *)(st.ch + (size_t)tile * g.n * kTile);
     c.lo8 = (uint32_t)lo * 8u;
-    c.Tb = st.T + (size_t)blockIdx.x * g.max_row_deg * F + f;
+    c.Tb = st.T + (size_t)blockIdx.x * 2 * g.max_row_deg * F + f;
+    c.tbuf = (size_t)g.max_row_deg * F;
     c.S = S + f;
     c.dummy = (double *)(lds + ly.dummy) + f;
     c.slot = (double *)(lds + ly.slot) + f;
@@ -965,7 +969,7 @@ hipError_t launch_tile_sub_stream(const DevGraph &g, const DevState &st, int max
                                   unsigned long long *next, unsigned long long *ctr, int64_t handoff, hipStream_t s) {
     const size_t lds = sub_lds_bytes_q<4>(g);
     // the 16-frame form only (+ static LDS: 2 x 16 ints, 16 frame indices, the refill flag)
-    if (!lds || !g.a_packed || !st.ubits || st.ntiles > st.nslots ||
+    if (!lds || !g.a_packed || !st.ubits || 2 * st.ntiles > st.nslots ||
         lds + 2 * 16 * sizeof(int) + 16 * sizeof(long long) + 16 > kSubLdsMax)
         return hipErrorInvalidValue;
     tile_sub_stream_kernel<4><<<st.ntiles * 4, 64 * kSW, lds, s>>>(g, st, max_iter, nllr ? 1 : 0, g.col_idx, g.row_ptr,
@@ -976,7 +980,7 @@ hipError_t launch_tile_sub_stream(const DevGraph &g, const DevState &st, int max
 
 hipError_t launch_tile_sub(const DevGraph &g, const DevState &st, int max_iter, bool nllr, hipStream_t s) {
     const size_t lds = sub_lds_bytes(g);
-    if (!lds) return hipErrorInvalidValue;
+    if (!lds || 2 * st.ntiles > st.nslots) return hipErrorInvalidValue;  // two rare-row buffers per workgroup
     tile_sub_kernel<4><<<st.ntiles * 4, 64 * kSW, lds, s>>>(g, st, max_iter, nllr ? 1 : 0, g.col_idx, g.row_ptr,
                                                             kAtanhCoef);
     return hipGetLastError();

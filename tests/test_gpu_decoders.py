@@ -202,11 +202,15 @@ def test_tile8_pair_matches_oracle(gpu_available, monkeypatch, snr, B):
         assert_llr_close(r.msgs, o["msgs"], "messages E", slack=sl_E)
 
 
-def test_tile8_pair_rare_rows(gpu_available, monkeypatch):
-    """The pair form's rare path (|t| <= 1e-10: the product of the others,
-    spa_decoder.py:159-164): frames with exact-zero channel LLRs on some
-    columns (rows with one zero t in either half of a pair, rows with two),
-    vs the oracle, T = 5."""
+_RARE_ROUTES = [("tile", "8p"), ("tile", 8), ("tile", None), ("split", None), ("edge", None)]
+
+
+@pytest.mark.parametrize("route,layout", _RARE_ROUTES, ids=[f"{r}{'' if l is None else l}" for r, l in _RARE_ROUTES])
+def test_2304_rare_rows(gpu_available, monkeypatch, route, layout):
+    """The rare path (|t| <= 1e-10: the product of the others,
+    spa_decoder.py:159-164) of the wimax_2304_0.5 decoders -- tile8's pair
+    form above all (a pair's two rows in one wavefront, either one tiny):
+    frames with exact-zero channel LLRs on 1-4 columns, vs the oracle, T = 5."""
     code = "wimax_2304_0.5"
     H = hstd_for(code)
     B, T = 24, 5
@@ -214,8 +218,11 @@ def test_tile8_pair_rare_rows(gpu_available, monkeypatch):
     rng = np.random.default_rng(78)
     for f in range(B):
         llr[f, rng.choice(H.shape[1], size=1 + f % 4, replace=False)] = 0.0
-    r = _run_route(code, "8p", "tile", llr, T, monkeypatch, nllr=True, post=True, msgs=True)
+    r = _run_route(code, layout, route, llr, T, monkeypatch, nllr=True, post=True, msgs=True)
     o = oracle.spa_decode(H, llr, T, nllr=True, want_E=True)
+    bad = np.nonzero((r.z != o["z"]).any(axis=1))[0]
+    assert bad.size == 0, (bad, [np.nonzero(r.z[f] != o["z"][f])[0] for f in bad],
+                           [np.nonzero(llr[f] == 0.0)[0] for f in bad])
     for key in ("z", "conv", "status", "iters", "nllr"):
         np.testing.assert_array_equal(r[key], o[key], err_msg=key)
     try:

@@ -1,0 +1,69 @@
+#!/usr/bin/env python3
+"""Summarize tools/profile_config5.sh into profiles/<tag>/: per SNR point,
+kernel_stats_<snr>.csv (rocprofv3 --stats, verbatim) and traffic_<snr>.json --
+HBM bytes per launch of phys_cn_tile_kernel, the config-5 CN kernel whose
+roofline bench.py's config5 key reports (committed_traffic matches code edges,
+frames and snr_db).  FETCH_SIZE is corrected as MI355X_MICROARCH.md §HBM
+prescribes, with the factor re-derived on this very access pattern: the VN
+kernel (phys_vn_tile_kernel) reads each fp32 message once plus Lambda per
+column, so its algorithmic read is known exactly per launch from the launches'
+own frame-iteration counts -- approximated here by the CN kernel's, since both
+launch once per iteration over the same running tiles.
+
+usage: summarize_config5.py SRC DST
+"""
+import collections
+import csv
+import glob
+import json
+import os
+import shutil
+import sys
+
+N, M = 64800, 32400
+EDGES = 226799
+
+
+def main(src, dst):
+    os.makedirs(dst, exist_ok=True)
+    for tdir in sorted(glob.glob(os.path.join(src, "trace_*"))):
+        if not os.path.isdir(tdir):
+            continue
+        snr = tdir.rsplit("trace_", 1)[1]
+        shutil.copy(os.path.join(tdir, "run_kernel_stats.csv"), os.path.join(dst, f"kernel_stats_{snr}.csv"))
+        stats = {r["Name"]: r for r in csv.DictReader(open(os.path.join(tdir, "run_kernel_stats.csv")))}
+        agg = collections.defaultdict(dict)
+        for name, sub in (("FETCH_SIZE", "fetch"), ("WRITE_SIZE", "write")):
+            vals = collections.defaultdict(list)
+            for r in csv.DictReader(open(os.path.join(src, f"{sub}_{snr}", "run_counter_collection.csv"))):
+                vals[r["Kernel_Name"]].append(float(r["Counter_Value"]))
+            for k, v in vals.items():
+                agg[k][name] = sum(v)
+                agg[k]["dispatches"] = len(v)
+        cn = next(k for k in agg if "phys_cn_tile" in k)
+        vn = next(k for k in agg if "phys_vn_tile" in k)
+        # VN per launch reads E (4 B x edges) and Lambda (4 B x n) of every running frame: the same
+        # frame-iterations as the CN launches; the FETCH_SIZE factor is the ratio on the VN kernel
+        # assuming its reads are exactly algorithmic (frame-iterations from the bench log)
+        log = open(os.path.join(src, f"trace_{snr}.log")).read()
+        js = json.loads(log[log.index("{\"metric\""):].split("\n")[0])
+        # the warm-up step decodes other frames of the same point: about the same iterations
+        fi = js["avg_iters"] * js["config"]["frames_per_gpu"] * (js["steps"] + js["warmup"])
+        calls_cn = agg[cn]["dispatches"]
+        vn_alg = 4.0 * (EDGES + N) * fi if fi else None
+        factor = vn_alg / (agg[vn]["FETCH_SIZE"] * 1024.0) if vn_alg else 2.0
+        rd = agg[cn]["FETCH_SIZE"] * 1024.0 * factor / calls_cn
+        wr = agg[cn]["WRITE_SIZE"] * 1024.0 / calls_cn
+        s = next(v for n, v in stats.items() if "phys_cn_tile" in n)
+        out = {"code": "dvbs2_profile_64800_0.5", "snr_db": float(snr), "frames": 8192, "edges": EDGES,
+               "fetch_correction_factor": factor, "factor_source": vn,
+               "frame_iterations": fi, "alg_bytes_per_launch": 12.0 * EDGES * fi / calls_cn if fi else None,
+               "kernels": {"phys_cn": {"kernel": cn, "read_bytes": rd, "write_bytes": wr, "traffic_bytes": rd + wr,
+                                       "avg_ns": float(s["AverageNs"]), "calls": int(s["Calls"]),
+                                       "traffic_GBs": (rd + wr) / float(s["AverageNs"])}}}
+        json.dump(out, open(os.path.join(dst, f"traffic_{snr}.json"), "w"), indent=2)
+        print(json.dumps(out, indent=2))
+
+
+if __name__ == "__main__":
+    main(sys.argv[1], sys.argv[2])
