@@ -103,7 +103,7 @@ struct T8Layout {
 };
 // R: rows of staged column indices per wavefront (D + 1: P3's row r-D+2 ..
 // the staged row r+2 of body(r+1))
-__host__ __device__ inline T8Layout t8_layout(int k, int m, int K, bool la, int R) {
+__host__ __device__ inline T8Layout t8_layout(int k, int m, int K, bool la, int R, int ns = kSR8) {
     T8Layout t;
     size_t o = 0;
     t.S = o;  // [k][8] column sums
@@ -112,16 +112,16 @@ __host__ __device__ inline T8Layout t8_layout(int k, int m, int K, bool la, int 
     if (la) o = al16(o + (size_t)k * kF8 * sizeof(double));
     t.math = o;
     o = al16(o + sizeof(MathLds));
-    t.slot = o;  // [kSR8][8] chain slots, then [kSR8][8] t of the identity edge
-    o = al16(o + 2 * kSR8 * (size_t)kF8 * sizeof(double));
+    t.slot = o;  // [ns][8] chain slots, then [ns][8] t of the identity edge
+    o = al16(o + 2 * (size_t)ns * kF8 * sizeof(double));
     t.zb = o;  // [kw][8] z^1 bits of the A columns
     o = al16(o + (size_t)((k + 31) / 32) * kF8 * sizeof(uint32_t));
     t.ib = o;  // [mw][8] z^1 bits of the identity columns
     o = al16(o + (size_t)((m + 31) / 32) * kF8 * sizeof(uint32_t));
     t.lane_i = o;  // bad[8], nllr count[8], live[8], it[8], fresh[8]
     o = al16(o + 5 * (size_t)kF8 * sizeof(int));
-    t.flags = o;  // chain flag[kSR8], tiny[kSR8], tiny sequence, running, p3row[16]
-    o = al16(o + (2 * kSR8 + 2 + kW8) * sizeof(int));
+    t.flags = o;  // chain flag[ns], tiny[ns], tiny sequence, running, p3row[16]
+    o = al16(o + (2 * (size_t)ns + 2 + kW8) * sizeof(int));
     t.dummy = o;  // [8] target of masked-off S updates
     o = al16(o + (size_t)kF8 * sizeof(double));
     t.cidx = o;  // [R][16][8*K] uint16 column indices, one wavefront chunk per row
@@ -129,6 +129,11 @@ __host__ __device__ inline T8Layout t8_layout(int k, int m, int K, bool la, int 
     t.total = o;
     return t;
 }
+
+// chain slots (rows) and index-ring rows of a variant: the row form kSR8 and
+// D + 1; the pair form 2 per chain slot (tp_slots) and 2 ring rows
+__host__ __device__ constexpr int t8_ns(bool pair, int D) { return pair ? 2 * 4 : kSR8; }
+__host__ __device__ constexpr int t8_ring(bool pair, int D) { return pair ? 2 : D + 1; }
 
 // deg: the whole row; the chunks cover its A edges (all but the last, the
 // identity column k + r at edge eid = beg + deg - 1).
@@ -169,12 +174,13 @@ struct T8Ctx {
     LdsTanh ttab;
     LdsAtanh ltab;
     AtanhCoef ac;
-    int m, k, wave, j, f;
+    int m, k, wave, j, f, nnz;
     int h;  // pair form: this lane's row of the pair (lane = h*32 + j*8 + f); 0 otherwise
     int ep0;
     bool first, live, fresh;
     int ntiny;
     int R;       // ring rows
+    int ns;      // chain slots (rows; pair form: 2 per pair)
     int idwave;  // the wavefront that owns the identity edge
 #ifdef LDPC_T8_TIMERS
     uint64_t tm[T8_NT];
@@ -605,8 +611,11 @@ __device__ __forceinline__ void t8_rows(T8Ctx<K> &c) {
 // just read (2 ring rows).  Chain slots: kPSR pairs x 2 halves in the same LDS
 // as the row form's kSR8 rows.
 constexpr int kPQ = 4;    // lane groups per row
-constexpr int kPSR = 4;   // chain slots (pairs): a slot is reused after every P3 of its pair (idwave = last)
-static_assert(2 * kPSR <= kSR8, "pair chain slots share the row form's LDS");
+// chain slots (pairs) of the pair form: a slot is reused only after every P3
+// of its pair (wavefront 0's P1(q) follows its P3(q-2), which waited for every
+// wavefront's hop(q-2), i.e. their P3(q-4)); 2 per pair in the layout
+template <int D>
+__host__ __device__ constexpr int tp_slots() { return 4; }
 
 struct PChunk {
     int deg, beg, c0, cnt, CS;  // this lane's row (per half)
@@ -677,14 +686,18 @@ __device__ __forceinline__ void tp_stage_commit(const T8Ctx<K> &c, int q, TpStag
 // P1 of pair q: t = tanh((L[col] - E_old)/2) of this lane's slots (L_A from
 // LDS); the identity edges' t (idwave) published in the pair's slot.  Returns
 // the rows' |t| <= 1e-10 votes: bit h = some live lane of half h.
-template <int K>
+// this lane's slot i column (the staged ring)
+template <int K, int D>
+__device__ __forceinline__ int tp_col(const T8Ctx<K> &c, int q, const PChunk &rc, int i) {
+    return tp_lcols(c, q, rc)[i];
+}
+template <int K, int D>
 __device__ __forceinline__ int tp_p1(const T8Ctx<K> &c, int q, double (&t)[K]) {
     const PChunk rc = tp_chunk(c, q);
     bool tiny = false;
     const int nj = tp_nj(c, rc);
     const int njt = c.live ? nj : 0;  // frame-less lanes abstain
     if (rc.any) {
-        const uint16_t *lc = tp_lcols(c, q, rc);
         const uint32_t eoff = ((uint32_t)(rc.c0 + c.j * rc.CS) << 6) + c.eo8;
         const bool noE = c.first || c.fresh;  // M = L - 0.0 == L: no E_old
         // E_old straight into t (all slots in flight); L[col] from LDS just
@@ -698,8 +711,8 @@ __device__ __forceinline__ int tp_p1(const T8Ctx<K> &c, int q, double (&t)[K]) {
                 t[i] = 1.0;
                 continue;
             }
-            const double Lc = c.LA[(size_t)lc[i] * kF8];   // L[col] (LDS)
-            const double M = noE ? Lc : Lc - t[i];  // :85-90 / :260-268
+            const double Lc = c.LA[(size_t)tp_col<K, D>(c, q, rc, i) * kF8];  // L[col] (LDS)
+            const double M = Lc - t[i];  // :85-90 / :260-268 (t = E_old, or +0.0 on a first pass: M == L bit for bit)
             const double tv = tanh_half_clipped(M, c.ttab);  // :138-146
             tiny |= i < njt && !(fabs(tv) > kTiny);
             t[i] = i < nj ? tv : 1.0;  // past the piece: an exact no-op in the product
@@ -716,7 +729,7 @@ __device__ __forceinline__ int tp_p1(const T8Ctx<K> &c, int q, double (&t)[K]) {
             const double eid = noE ? 0.0 : t8_ld<kNT>(c.rE, ((uint32_t)(rc.beg + rc.deg - 1) << 6) + c.eo8);
             const double tv = tanh_half_clipped(noE ? lid : lid - eid, c.ttab);
             tiny |= c.live && !(fabs(tv) > kTiny);
-            if (c.j == 0) c.slot[(kSR8 + (q & (kPSR - 1)) * 2 + c.h) * kF8] = tv;
+            if (c.j == 0) c.slot[(c.ns + (q & (tp_slots<D>() - 1)) * 2 + c.h) * kF8] = tv;
         }
     }
     const unsigned long long b = __ballot(tiny);
@@ -724,16 +737,19 @@ __device__ __forceinline__ int tp_p1(const T8Ctx<K> &c, int q, double (&t)[K]) {
 }
 
 // hop of pair q: this wavefront's chunks of both rows' left-to-right products.
-template <int K>
+template <int K, int D>
 __device__ __forceinline__ void tp_hop(T8Ctx<K> &c, int q, const double (&t)[K], int tiny) {
-    const int s = q & (kPSR - 1);
+    const int s = q & (tp_slots<D>() - 1);
     const int ep = ((c.ep0 + q) & 0x3ffffff) * 32;
     double *sl = c.slot + (s * 2 + c.h) * kF8;
     double P = 1.0;  // 1.0 * t0 == t0 exactly
+    T8_STAMP(h0);
     if (c.wave != 0) {
         wait_flag<false>(c.flag + s, ep + c.wave);
         P = *sl;
     }
+    T8_STAMP(h1);
+    T8_ADD(c, 0, h0, h1);
     __builtin_amdgcn_s_setprio(2);
     if (uniform(tp_chunk(c, q).any ? 1 : 0)) {
         // branch-free: every group multiplies all K slots (1.0-padded: exact
@@ -759,6 +775,8 @@ __device__ __forceinline__ void tp_hop(T8Ctx<K> &c, int q, const double (&t)[K],
     lds_release();
     if ((threadIdx.x & 63) == 0) lds_st(c.flag + s, ep + c.wave + 1);
     __builtin_amdgcn_s_setprio(0);
+    T8_STAMP(h2);
+    T8_ADD(c, 1, h1, h2);
 }
 
 // Row r's S additions may start once the wavefronts whose column spans
@@ -775,27 +793,28 @@ __device__ __forceinline__ void tp_order(const T8Ctx<K> &c, int r) {
 // row 2q then row 2q+1 in the column order; the identity columns' posteriors
 // and z^1 bits.  The indices of pair q+2 (staged by the caller) replace this
 // pair's ring row once read.
-template <int K>
+template <int K, int D>
 __device__ __forceinline__ void tp_p3(T8Ctx<K> &c, int q, double (&t)[K], TpStage nxt) {
     const PChunk rc = tp_chunk(c, q);
-    const int s = q & (kPSR - 1);
+    const int s = q & (tp_slots<D>() - 1);
     const int ep = ((c.ep0 + q) & 0x3ffffff) * 32;
     const int r = 2 * q + c.h;
     const bool idw = c.wave == c.idwave && rc.deg > 0;  // this lane holds its row's identity edge
     double chI = 0.0;
     if (idw) chI = t8_ld(c.rC, ((uint32_t)(c.k + r) << 9) + c.lo8);  // for L = ch + (0 + E)
+    // this pair's staged columns; its ring row takes pair q+2's next
     int col[K];
-    {
-        const uint16_t *lc = tp_lcols(c, q, rc);
 #pragma unroll
-        for (int i = 0; i < K; ++i) col[i] = lc[i];
-    }
+    for (int i = 0; i < K; ++i) col[i] = tp_col<K, D>(c, q, rc, i);
     tp_stage_commit(c, q + 2, nxt);  // the ring row is read (in-order LDS of this wavefront)
+    T8_STAMP(q0);
     wait_flag<false>(c.flag + s, ep + kW8);  // both rows' A products are complete
+    T8_STAMP(q1);
+    T8_ADD(c, 2, q0, q1);
     const bool tiny_row = lds_ld(c.tinyf + s * 2 + c.h) != 0;
     const bool tiny_any = __ballot(tiny_row) != 0ull;
     const int nj = tp_nj(c, rc);
-    const double tI = c.slot[(kSR8 + s * 2 + c.h) * kF8];
+    const double tI = c.slot[(c.ns + s * 2 + c.h) * kF8];
     const double P = c.slot[(s * 2 + c.h) * kF8] * tI;  // (t_0 * ... * t_{deg-2}) * t_id: left to right
     // E_new stored (slots past the piece and frames that stopped store out of
     // range: dropped); S_col += E_new row 2q then row 2q+1 in the column
@@ -811,7 +830,11 @@ __device__ __forceinline__ void tp_p3(T8Ctx<K> &c, int q, double (&t)[K], TpStag
         // S_col += E_new; slots past the piece add into `dummy` (never read)
         auto sp = [&](int i) { return i < nj ? c.S + (size_t)col[i] * kF8 : c.dummy; };
         // row 2q: half 0's additions after the overlapping wavefronts' row 2q-1
+        T8_STAMP(f0);
+        T8_ADD(c, 3, q1, f0);
         tp_order(c, 2 * q);
+        T8_STAMP(f1);
+        T8_ADD(c, 4, f0, f1);
         if (c.h == 0) {
 #pragma unroll
             for (int i = 0; i < K; ++i) __hip_atomic_fetch_add(sp(i), tt[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -819,7 +842,11 @@ __device__ __forceinline__ void tp_p3(T8Ctx<K> &c, int q, double (&t)[K], TpStag
         lds_release();
         if ((threadIdx.x & 63) == 0) lds_st(c.p3row + c.wave, 2 * q + 1);
         // row 2q+1: half 1's, after the overlapping wavefronts' row 2q
+        T8_STAMP(f2);
+        T8_ADD(c, 5, f1, f2);
         tp_order(c, 2 * q + 1);
+        T8_STAMP(f3);
+        T8_ADD(c, 4, f2, f3);
         if (c.h == 1) {
 #pragma unroll
             for (int i = 0; i < K; ++i) __hip_atomic_fetch_add(sp(i), tt[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -831,6 +858,8 @@ __device__ __forceinline__ void tp_p3(T8Ctx<K> &c, int q, double (&t)[K], TpStag
         }
         lds_release();
         if ((threadIdx.x & 63) == 0) lds_st(c.p3row + c.wave, 2 * q + 2);
+        T8_STAMP(f4);
+        T8_ADD(c, 5, f3, f4);
     };
     if (!tiny_any) {
         // q = P/t (div_nr where exact), then E_new = 2 atanh(clip(q)), or 2q
@@ -921,32 +950,37 @@ __device__ __forceinline__ void tp_p3(T8Ctx<K> &c, int q, double (&t)[K], TpStag
     }
 }
 
-// body(q) = hop(q), P3(q-1) (staging pair q+1), P1(q+1)
+// D = 2: body(q) = hop(q), P3(q-1) (staging pair q+1), P1(q+1)
 template <int K>
-__device__ __forceinline__ void tp_body(T8Ctx<K> &c, int q, int mp, double (&tc)[K], int yc, double (&to)[K],
-                                        int &yo) {
-    if (q < mp) tp_hop(c, q, tc, yc);
-    if (q >= 1) tp_p3(c, q - 1, to, tp_stage_issue(c, q + 1));
-    if (q + 1 < mp) yo = tp_p1(c, q + 1, to);
+__device__ __forceinline__ void tp_body2(T8Ctx<K> &c, int q, int mp, double (&tc)[K], int yc, double (&to)[K],
+                                         int &yo) {
+    if (q < mp) tp_hop<K, 2>(c, q, tc, yc);
+    T8_STAMP(b0);
+    if (q >= 1) tp_p3<K, 2>(c, q - 1, to, tp_stage_issue(c, q + 1));
+    T8_STAMP(b1);
+    if (q + 1 < mp) yo = tp_p1<K, 2>(c, q + 1, to);
+    T8_STAMP(b2);
+    T8_ADD(c, 6, b1, b2);
+    T8_ADD(c, 7, b0, b1);
 }
-
 // One pass over all row pairs (every P3 done on return, before the barrier).
-template <int K>
+template <int K, int D>
 __device__ __forceinline__ void tp_rows(T8Ctx<K> &c) {
     const int mp = (c.m + 1) / 2;  // pairs (an odd m's last pair has an empty second row)
     if (mp <= 0) return;
+    static_assert(D == 2, "the pair form runs two pairs in flight (three measured 0.31 vs 0.41: spills)");
     double tA[K], tB[K];
     int yA = 0, yB = 0;
     tp_stage_commit(c, 0, tp_stage_issue(c, 0));
     tp_stage_commit(c, 1, tp_stage_issue(c, 1));
-    yA = tp_p1(c, 0, tA);
+    yA = tp_p1<K, 2>(c, 0, tA);
     for (int q = 0; q <= mp; q += 2) {
-        tp_body(c, q, mp, tA, yA, tB, yB);
-        if (q + 1 <= mp) tp_body(c, q + 1, mp, tB, yB, tA, yA);
+        tp_body2(c, q, mp, tA, yA, tB, yB);
+        if (q + 1 <= mp) tp_body2(c, q + 1, mp, tB, yB, tA, yA);
     }
 }
 
-template <int K, bool LA, bool PAIR>
+template <int K, bool LA, bool PAIR, int NS>
 __device__ __forceinline__ void t8_setup(T8Ctx<K> &c, unsigned char *lds, const T8Layout &ly, const DevGraph &g,
                                          const DevState &st, int tile, int sub, const int *col_idx,
                                          const int *row_ptr, const AtanhCoef &ac) {
@@ -978,14 +1012,16 @@ __device__ __forceinline__ void t8_setup(T8Ctx<K> &c, unsigned char *lds, const 
     c.ib = (uint32_t *)(lds + ly.ib) + c.f;
     c.cidx = (uint16_t *)(lds + ly.cidx) + c.wave * kQ8 * K;
     c.flag = flags;
-    c.tinyf = flags + kSR8;
-    c.tseq = flags + 2 * kSR8;
-    c.p3row = flags + 2 * kSR8 + 2;
+    c.ns = NS;
+    c.tinyf = flags + NS;
+    c.tseq = flags + 2 * NS;
+    c.p3row = flags + 2 * NS + 2;
     c.ttab = LdsTanh{mlds.tanh};
     c.ltab = LdsAtanh{mlds.atanh};
     c.ac = ac;
     c.m = g.m;
     c.k = g.k;
+    c.nnz = g.nnz;
     c.ntiny = 0;
     c.first = false;
     c.fresh = false;
@@ -1055,7 +1091,8 @@ __global__ __launch_bounds__(64 * kW8, 1) void tile8_kernel(DevGraph g, DevState
                                                             const int *__restrict__ col_idx,
                                                             const int *__restrict__ row_ptr, AtanhCoef ac) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
-    const T8Layout ly = t8_layout(g.k, g.m, K, LA, PAIR ? 2 : D + 1);
+    constexpr int NS = t8_ns(PAIR, D);
+    const T8Layout ly = t8_layout(g.k, g.m, K, LA, t8_ring(PAIR, D), NS);
     double *S = (double *)(lds + ly.S);
     double *LAl = LA ? (double *)(lds + ly.LA) : nullptr;
     uint32_t *zb = (uint32_t *)(lds + ly.zb);
@@ -1072,8 +1109,8 @@ __global__ __launch_bounds__(64 * kW8, 1) void tile8_kernel(DevGraph g, DevState
     for (int i = threadIdx.x; i < g.k * kF8; i += blockDim.x) S[i] = 0.0;
     for (int i = threadIdx.x; i < (kw + mw) * kF8; i += blockDim.x) zb[i] = 0u;
     for (int i = threadIdx.x; i < 2 * kF8; i += blockDim.x) bad[i] = 0;
-    if (threadIdx.x < 2 * kSR8) flags[threadIdx.x] = -1;
-    if (threadIdx.x >= 2 * kSR8 && threadIdx.x < 2 * kSR8 + 2 + kW8) flags[threadIdx.x] = 0;
+    if (threadIdx.x < 2 * NS) flags[threadIdx.x] = -1;
+    if (threadIdx.x >= 2 * NS && threadIdx.x < 2 * NS + 2 + kW8) flags[threadIdx.x] = 0;
     const int lane = threadIdx.x & 63;
     if (threadIdx.x < kF8) livel[threadIdx.x] = st.done[tile * kTile + sub * kF8 + threadIdx.x] == 0 ? 1 : 0;
     const __amdgpu_buffer_rsrc_t rC = t8_rsrc(st.ch + (size_t)tile * g.n * kTile, (size_t)g.n * kTile * sizeof(double));
@@ -1092,12 +1129,15 @@ __global__ __launch_bounds__(64 * kW8, 1) void tile8_kernel(DevGraph g, DevState
     }
 
     T8Ctx<K> c;
-    t8_setup<K, LA, PAIR>(c, lds, ly, g, st, tile, sub, col_idx, row_ptr, ac);
-    c.R = PAIR ? 2 : D + 1;
+    t8_setup<K, LA, PAIR, NS>(c, lds, ly, g, st, tile, sub, col_idx, row_ptr, ac);
+    c.R = t8_ring(PAIR, D);
     // the identity edge's wavefront: with D = 3 wavefront 0, which otherwise
     // waits longest for the chain; with D = 2 the last one (wavefront 0's
     // body would bound the row period)
-    c.idwave = D >= 3 && !PAIR ? 0 : kW8 - 1;
+    // the identity edge(s) on wavefront 0, first in the chain: the last one's
+    // extra P1/P3 work sat on the chain's tail (config 4 static 0.381 -> 0.396,
+    // pair form +2.9 %, profiles/r5l_ab, r5m_ab)
+    c.idwave = 0;
     const int fr = tile * kTile + sub * kF8 + c.f;  // this lane's frame
 
     for (int it = 0; it < max_iter; ++it) {
@@ -1106,7 +1146,7 @@ __global__ __launch_bounds__(64 * kW8, 1) void tile8_kernel(DevGraph g, DevState
         c.ep0 = t8_epoch0(it, g.m);
         T8_STAMP(w0);
         if constexpr (PAIR)
-            tp_rows<K>(c);
+            tp_rows<K, D>(c);
         else
             t8_rows<K, LA, D>(c);
         T8_STAMP(w1);
@@ -1146,11 +1186,11 @@ __global__ __launch_bounds__(64 * kW8, 1) void tile8_kernel(DevGraph g, DevState
                 bad[lane] = 0;
                 cntl[lane] = 0;
             }
-            if (lane == 0) flags[2 * kSR8 + 1] = any != 0ull ? 1 : 0;
+            if (lane == 0) flags[2 * NS + 1] = any != 0ull ? 1 : 0;
         }
         for (int i = threadIdx.x; i < (kw + mw) * kF8; i += blockDim.x) zb[i] = 0u;
         __syncthreads();
-        if (!flags[2 * kSR8 + 1]) break;
+        if (!flags[2 * NS + 1]) break;
     }
 #ifdef LDPC_T8_TIMERS
     if ((blockIdx.x == 0 || blockIdx.x == 777) && (threadIdx.x & 63) == 0)
@@ -1184,7 +1224,8 @@ __global__ __launch_bounds__(64 * kW8, 1) void tile8_stream_kernel(
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     __shared__ long long gidx[kF8];  // refill: slot f's new frame index (< 0: none)
     __shared__ int nref;             // refill: some slot took a frame this pass
-    const T8Layout ly = t8_layout(g.k, g.m, K, LA, PAIR ? 2 : D + 1);
+    constexpr int NS = t8_ns(PAIR, D);
+    const T8Layout ly = t8_layout(g.k, g.m, K, LA, t8_ring(PAIR, D), NS);
     double *S = (double *)(lds + ly.S);
     double *LAl = LA ? (double *)(lds + ly.LA) : nullptr;
     uint32_t *zb = (uint32_t *)(lds + ly.zb);
@@ -1203,8 +1244,8 @@ __global__ __launch_bounds__(64 * kW8, 1) void tile8_stream_kernel(
     for (int i = threadIdx.x; i < g.k * kF8; i += blockDim.x) S[i] = 0.0;
     for (int i = threadIdx.x; i < (kw + mw) * kF8; i += blockDim.x) zb[i] = 0u;
     if (threadIdx.x < 5 * kF8) bad[threadIdx.x] = 0;  // bad, cnt, live, it, fresh
-    if (threadIdx.x < 2 * kSR8) flags[threadIdx.x] = -1;
-    if (threadIdx.x >= 2 * kSR8 && threadIdx.x < 2 * kSR8 + 2 + kW8) flags[threadIdx.x] = 0;
+    if (threadIdx.x < 2 * NS) flags[threadIdx.x] = -1;
+    if (threadIdx.x >= 2 * NS && threadIdx.x < 2 * NS + 2 + kW8) flags[threadIdx.x] = 0;
     const int lane = threadIdx.x & 63;
     const bool w0 = (threadIdx.x >> 6) == 0;        // hardware wavefront 0 runs the refill and the exits
     const bool slot_lane = threadIdx.x < kF8;       // the lane that owns frame slot f = lane
@@ -1213,9 +1254,9 @@ __global__ __launch_bounds__(64 * kW8, 1) void tile8_stream_kernel(
     const __amdgpu_buffer_rsrc_t rL = t8_rsrc(st.L + (size_t)tile * g.n * kTile, (size_t)g.n * kTile * sizeof(double));
 
     T8Ctx<K> c;
-    t8_setup<K, LA, PAIR>(c, lds, ly, g, st, tile, sub, col_idx, row_ptr, ac);
-    c.R = PAIR ? 2 : D + 1;
-    c.idwave = D >= 3 && !PAIR ? 0 : kW8 - 1;  // as tile8_kernel
+    t8_setup<K, LA, PAIR, NS>(c, lds, ly, g, st, tile, sub, col_idx, row_ptr, ac);
+    c.R = t8_ring(PAIR, D);
+    c.idwave = 0;  // as tile8_kernel
     const int m = g.m;
     const uint32_t *Ut = st.ubits + (size_t)tile * kw * kTile + sub * kF8 + lane;  // slot lanes only
 
@@ -1260,12 +1301,12 @@ __global__ __launch_bounds__(64 * kW8, 1) void tile8_stream_kernel(
                 st.refill[fr] = 0;
             }
             if (lane == 0) {
-                flags[2 * kSR8 + 1] = go ? 1 : 0;
+                flags[2 * NS + 1] = go ? 1 : 0;
                 nref = go && gen ? 1 : 0;
             }
         }
         __syncthreads();
-        if (!flags[2 * kSR8 + 1]) break;  // supply exhausted (or handed off), every slot drained
+        if (!flags[2 * NS + 1]) break;  // supply exhausted (or handed off), every slot drained
         if (nref) {  // the new frames, generated by the whole workgroup (u bits staged in zb)
             gen_slots<kF8>(g, st, tile, sub * kF8, gidx, zb, seed, snr_point, sigma);
             if constexpr (LA) {  // a new frame's first pass gathers L = ch
@@ -1280,7 +1321,7 @@ __global__ __launch_bounds__(64 * kW8, 1) void tile8_stream_kernel(
         c.first = false;
         c.ep0 = t8_epoch0(pass, m);
         if constexpr (PAIR)
-            tp_rows<K>(c);
+            tp_rows<K, D>(c);
         else
             t8_rows<K, LA, D>(c);
         __syncthreads();  // every P3 done: S complete, identity bits set
@@ -1340,14 +1381,14 @@ size_t t8_lds_bytes_k(const DevGraph &g) {
     if (!g.std_form || !g.a_packed || g.k <= 0 || g.n > 65535) return 0;
     const int C = (g.max_row_deg + kW8 - 1) / kW8;
     if ((C + (PAIR ? kPQ : kQ8) - 1) / (PAIR ? kPQ : kQ8) > K) return 0;
-    const size_t b = t8_layout(g.k, g.m, K, LA, PAIR ? 2 : D + 1).total;
+    const size_t b = t8_layout(g.k, g.m, K, LA, t8_ring(PAIR, D), t8_ns(PAIR, D)).total;
     return b + 16 <= kLds8Max ? b : 0;  // + the static __shared__ counter(s)
 }
 
 // the variant a graph runs: 0 = none, else K * 2 + LA (+ 100: the pair form,
 // DevGraph::t8pair, chosen at graph creation)
 int t8_variant(const DevGraph &g) {
-    if (g.t8pair && t8_lds_bytes_k<10, true, 2, true>(g)) return 100 + 10 * 2 + 1;
+    if (g.t8pair && t8_lds_bytes_k<10, true, 2, true>(g)) return 121;
     if (t8_lds_bytes_k<5, true, kD5>(g)) return 5 * 2 + 1;
     if (t8_lds_bytes_k<8, false, kD8>(g)) return 8 * 2;
     return 0;

@@ -54,6 +54,17 @@ namespace {
 // wavefronts per workgroup: kSubWaves (16, spa_device.h; 12 wavefronts with
 // 168 registers each spilled less but measured 6 % slower, profiles/r4z_ab)
 constexpr int kSW = kSubWaves;
+// -DLDPC_SUB_TIMERS: diagnostic build (never the product) -- s_memtime phase
+// timers per wavefront, printed for two workgroups at the end of the launch:
+// hop wait, hop, P3 chain wait, P3 math + stores, P3 order wait, P3 adds, P1
+#ifdef LDPC_SUB_TIMERS
+#define SUB_NT 7
+#define SUB_STAMP(v) const uint64_t v = __builtin_amdgcn_s_memtime()
+#define SUB_ADD(c, i, a, b) ((c).tm[i] += (b) - (a))
+#else
+#define SUB_STAMP(v)
+#define SUB_ADD(c, i, a, b)
+#endif
 constexpr size_t kSubLdsMax = 163840;
 
 template <int Q>
@@ -176,6 +187,9 @@ struct SubCtx {
     bool first, live;
     bool fresh;  // streaming: this lane's frame is on its first pass (M = L - 0, L = ch)
     int ntiny;
+#ifdef LDPC_SUB_TIMERS
+    mutable uint64_t tm[SUB_NT];
+#endif
 };
 
 // this lane's edge count in chunk rc, and the edge of its slot i (clamped
@@ -351,10 +365,13 @@ __device__ __forceinline__ void sub_hop(const SubCtx<Q> &c, int r, const double 
     const int ep = ((c.ep0 + r) & 0x3ffffff) * 32;
     double *sl = c.slot + s * F;
     double P = 1.0;  // 1.0 * t0 == t0 exactly
+    SUB_STAMP(h0);
     if (c.wave != 0) {
         wait_flag<false>(c.flag + s, ep + c.wave);
         P = *sl;
     }
+    SUB_STAMP(h1);
+    SUB_ADD(c, 0, h0, h1);
     __builtin_amdgcn_s_setprio(2);
     int last = -1;
     if (Q == 4 && rc.cnt > 0) {
@@ -392,10 +409,20 @@ __device__ __forceinline__ void sub_hop(const SubCtx<Q> &c, int r, const double 
     lds_release();
     if ((threadIdx.x & 63) == 0) lds_st(c.flag + s, ep + c.wave + 1);
     __builtin_amdgcn_s_setprio(0);
+    SUB_STAMP(h2);
+    SUB_ADD(c, 1, h1, h2);
 }
 
 // P3: E_new of this lane's slots of row r, stored and folded into S; the
 // identity column's posterior and z^1 bit.
+// row r-1's P3 by the wavefronts whose column spans overlap this one's (sub_p3)
+template <int Q>
+__device__ __forceinline__ void sub_order(const SubCtx<Q> &c, int r) {
+    if (r > 0) {
+        const int d = c.p3dep[r * kSW + c.wave];
+        for (int v = d & 0xff; v <= (d >> 8); ++v) wait_ge<false>(c.p3row + v, r);
+    }
+}
 template <int Q>
 __device__ __forceinline__ void sub_p3_body(SubCtx<Q> &c, int r, double (&t)[SubCfg<Q>::K]) {
     constexpr int F = SubCfg<Q>::F, K = SubCfg<Q>::K;
@@ -403,9 +430,21 @@ __device__ __forceinline__ void sub_p3_body(SubCtx<Q> &c, int r, double (&t)[Sub
     if (rc.deg == 0) return;
     const int s = r & (kSR - 1);
     const int ep = ((c.ep0 + r) & 0x3ffffff) * 32;
+    // the identity column k + r is the row's last edge (an [A | I] graph):
+    // the lane whose piece ends there requests its channel LLR now, ahead of
+    // the chain wait (+1 % with the late S-order wait below, profiles/r5n_ab)
+    double chI = 0.0;
+    {
+        const int njI = sub_nj(c, rc);
+        if (njI > 0 && rc.c0 + c.j * rc.CS + njI == c.row_ptr[r + 1]) chI = *sub_c(c, c.k + r);
+    }
+    SUB_STAMP(q0);
     wait_flag<false>(c.flag + s, ep + kSW);
+    SUB_STAMP(q1);
+    SUB_ADD(c, 2, q0, q1);
     const bool tiny_row = uniform(lds_ld(c.tinyf + s)) != 0;
     if (rc.cnt == 0) {  // no edges here (short rows): still take part in a rare row's parking count
+        sub_order(c, r);
         if (tiny_row) {
             c.ntiny += 1;
             if ((threadIdx.x & 63) == 0)
@@ -507,17 +546,26 @@ __device__ __forceinline__ void sub_p3_body(SubCtx<Q> &c, int r, double (&t)[Sub
             colI = col[i];
         }
     }
+    // S order: only the additions wait for the overlapping wavefronts' row
+    // r-1 (the math and the E_new stores above run meanwhile)
+    SUB_STAMP(q2);
+    SUB_ADD(c, 3, q1, q2);
+    sub_order(c, r);
+    SUB_STAMP(q3);
+    SUB_ADD(c, 4, q2, q3);
 #pragma unroll
     for (int i = 0; i < K; ++i)  // one ds_add_f64 per slot; slots past the piece add into `dummy` (never read)
         __hip_atomic_fetch_add(sp[i], t[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     if (colI >= 0) {  // identity column: L = ch + (0 + E) (:173-185)
-        const double Lj = *sub_c(c, colI) + (0.0 + EnI);
+        const double Lj = chI + (0.0 + EnI);
         if (c.live) *sub_l(c, colI) = Lj;
         if (!(Lj < 0.0)) {
             const int q = colI - c.k;
             atomicOr(c.ib + (q >> 5) * F, 1u << (q & 31));
         }
     }
+    SUB_STAMP(q4);
+    SUB_ADD(c, 5, q3, q4);
 }
 
 // P3 of row r.  S_col must take its additions rows ascending.  Wavefront w's
@@ -533,10 +581,6 @@ __device__ __forceinline__ void sub_p3_body(SubCtx<Q> &c, int r, double (&t)[Sub
 // many passes a streaming launch makes.
 template <int Q>
 __device__ __forceinline__ void sub_p3(SubCtx<Q> &c, int r, double (&t)[SubCfg<Q>::K]) {
-    if (r > 0) {  // row r-1's P3 by the wavefronts whose column spans overlap ours
-        const int d = c.p3dep[r * kSW + c.wave];
-        for (int v = d & 0xff; v <= (d >> 8); ++v) wait_ge<false>(c.p3row + v, r);
-    }
     sub_p3_body<Q>(c, r, t);
     lds_release();  // this row's S additions before the count
     if ((threadIdx.x & 63) == 0)
@@ -558,7 +602,10 @@ __device__ __forceinline__ void sub_body(SubCtx<Q> &c, int r, int m, double (&tc
                                          double (&toth)[SubCfg<Q>::K], bool &yoth) {
     if (r < m) sub_hop(c, r, tcur, ycur);
     if (r >= 1) sub_p3<Q>(c, r - 1, toth);
+    SUB_STAMP(p0);
     if (r + 1 < m) yoth = sub_p1<Q>(c, r + 1, sub_chunk(c.row_ptr, r + 1, c.wave, Q), toth);
+    SUB_STAMP(p1);
+    SUB_ADD(c, 6, p0, p1);
 }
 
 template <int Q>
@@ -633,6 +680,9 @@ __global__ __launch_bounds__(64 * kSW, 1) void tile_sub_kernel(DevGraph g, DevSt
     c.f = f;
     c.ntiny = 0;
     c.fresh = false;
+#ifdef LDPC_SUB_TIMERS
+    for (int i = 0; i < SUB_NT; ++i) c.tm[i] = 0;
+#endif
     const int m = g.m;
     const int nthr = kSW * Q;       // (wavefront, lane group) pairs
     const int me = wave * Q + j;    // this lane's pair
@@ -721,6 +771,13 @@ __global__ __launch_bounds__(64 * kSW, 1) void tile_sub_kernel(DevGraph g, DevSt
         __syncthreads();
         if (!flags[2 * kSR + 1]) break;
     }
+#ifdef LDPC_SUB_TIMERS
+    if ((blockIdx.x == 0 || blockIdx.x == 777) && (threadIdx.x & 63) == 0)
+        printf("SUB b=%d w=%d hopw=%llu hop=%llu p3f=%llu p3m=%llu p3o=%llu p3s=%llu p1=%llu\n", (int)blockIdx.x,
+               c.wave, (unsigned long long)c.tm[0], (unsigned long long)c.tm[1], (unsigned long long)c.tm[2],
+               (unsigned long long)c.tm[3], (unsigned long long)c.tm[4], (unsigned long long)c.tm[5],
+               (unsigned long long)c.tm[6]);
+#endif
 }
 
 // Streaming Monte-Carlo on sub-tiles (tile_kernels.hip's tile_stream_kernel,

@@ -76,7 +76,7 @@ def _graph(code, layout, monkeypatch):
     if key not in _GRAPHS:
         if layout is not None:
             monkeypatch.setenv("LDPC_TILE8", "0" if layout == 64 else "1")
-        if layout == "8p":
+        if layout == "8p":  # tile8's pair form (two rows per wavefront)
             monkeypatch.setenv("LDPC_T8_PAIR", "1")
         try:
             _GRAPHS[key] = Graph(hstd_for(code))
@@ -177,11 +177,11 @@ def test_tile8_matches_oracle_config4_sweep(gpu_available, monkeypatch, code, sn
         assert (r.status == 1).mean() > 0.9  # the reference's own cliff (golden w2304A_T3_4dB)
 
 
-_PAIR = [(s, n) for s in (1.0, 2.0, 3.0) for n in (72,)] + [(2.0, 130)]
+_PAIR = [(s, n, "8p") for s in (1.0, 2.0, 3.0) for n in (72,)] + [(2.0, 130, "8p")]
 
 
-@pytest.mark.parametrize("snr,B", _PAIR, ids=[f"{s}dB-{n}" for s, n in _PAIR])
-def test_tile8_pair_matches_oracle(gpu_available, monkeypatch, snr, B):
+@pytest.mark.parametrize("snr,B,layout", _PAIR, ids=[f"{l}-{s}dB-{n}" for s, n, l in _PAIR])
+def test_tile8_pair_matches_oracle(gpu_available, monkeypatch, snr, B, layout):
     """tile8's pair form (two rows per wavefront, wimax_2304_0.5) vs the oracle
     at T=50: 72 frames (one full tile + one live 8-frame sub-tile) and 130
     (two full tiles + a 2-frame sub-tile)."""
@@ -189,7 +189,7 @@ def test_tile8_pair_matches_oracle(gpu_available, monkeypatch, snr, B):
     H = hstd_for(code)
     T = 50
     llr = _random_llr(H, B, snr, seed=5100 + int(10 * snr) + B)
-    r = _run_route(code, "8p", "tile", llr, T, monkeypatch, nllr=True, post=True, msgs=True)
+    r = _run_route(code, layout, "tile", llr, T, monkeypatch, nllr=True, post=True, msgs=True)
     o = oracle.spa_decode(H, llr, T, nllr=True, want_E=True)
     for key in ("z", "conv", "status", "iters", "nllr"):
         np.testing.assert_array_equal(r[key], o[key], err_msg=key)
