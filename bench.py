@@ -94,7 +94,7 @@ def parse():
                     help="parity mode: a second physical-mode point in the waterfall, where the decoder "
                          "iterates (reported under physical.waterfall; NaN = none)")
     ap.add_argument("--phys-frames", type=int, default=262144,
-                    help="frames per physical-mode step (config 3's batch; 65,536 measured 2.7 % slower: host syncs)")
+                    help="frames per physical-mode step (config 3's batch; 65,536 measured 2.7 %% slower: host syncs)")
     ap.add_argument("--config4-snr", default="1.0:0.5:4.0",
                     help="parity mode: BASELINE config 4's Eb/N0 sweep (start:step:end, main.py's grid) on "
                          "--config4-code, reported under 'config4' ('' = none)")
