@@ -38,6 +38,12 @@ __device__ __forceinline__ void wait_ge(const int *p, int v) {
         if (kSleep) __builtin_amdgcn_s_sleep(1);
     lds_acquire();
 }
+// A read-only table entry at a wavefront-uniform index by a scalar load (SMEM,
+// lgkmcnt): the vector load's vmcnt wait would also wait for every store the
+// wavefront has in flight (the P3 order tables: this row's E_new stores).
+__device__ __forceinline__ int ld_table(const int *p, int i) {
+    return *(const __attribute__((address_space(4))) int *)(p + uniform(i));
+}
 // Load through L2 (not this CU's L1): data another wavefront of the workgroup
 // stored (posteriors, rare-row scratch).
 __device__ __forceinline__ double ld_l2(const double *p) {

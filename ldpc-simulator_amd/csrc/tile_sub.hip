@@ -104,8 +104,25 @@ constexpr int kSR = 4;  // chain slots
 // streaming (profiles/r2at_wave_map; pairs of positions per SIMD measured the
 // same, spin waits at a lower issue priority +0.2 %).
 __device__ __forceinline__ int sub_wave(int hw) { return (hw & 3) * (kSW / 4) + (hw >> 2); }
-__device__ __forceinline__ double ld_sub_msg(const double *p) { return __builtin_nontemporal_load(p); }
-__device__ __forceinline__ void st_sub_msg(double *p, double v) { __builtin_nontemporal_store(v, p); }
+// E_new stores through a buffer resource: a slot past the lane's piece (or a
+// frame-less lane) stores at kSubOOB, past num_records, which the hardware
+// drops -- no branch per slot, so every memory operation of the row loop is
+// unconditional and the compiler's vmcnt waits count exactly (with branches
+// it waited for this row's stores before P1's first request)
+typedef unsigned int sub_u2 __attribute__((ext_vector_type(2)));
+constexpr uint32_t kSubOOB = 0xfffffff0u;
+__device__ __forceinline__ void st_sub_msg(__amdgpu_buffer_rsrc_t r, uint32_t off, double v) {
+    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(sub_u2, v), r, off, 0, 2 /* nt */);
+}
+// E_old loads the same way: at kSubOOB (iteration 0, a fresh frame) the
+// hardware returns 0 without a memory request
+__device__ __forceinline__ double ld_sub_msg(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+    return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 2 /* nt */));
+}
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t sub_rsrc(const void *base, size_t bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(base), (short)0, (int)min(bytes, (size_t)0x7fffffff),
+                                            0x00020000);
+}
 
 // Column indices of the rows in flight, staged per wavefront in LDS as 16-bit
 // values one row ahead of their P1 (a ring of 3 rows: P3(r-1), P1(r+1) and the
@@ -181,6 +198,7 @@ struct SubCtx {
     // uniform (SGPR) tile bases + this lane's byte offset: every access is a
     // 32-bit per-lane offset from a scalar base (global_load ... v_off, s_base)
     const char *Eu, *Lu, *Cu;
+    __amdgpu_buffer_rsrc_t rE;  // the tile's E for masked stores without a branch (sub_p3_body)
     uint32_t lo8;
     int k, wave, j, f;
     int ep0;
@@ -228,29 +246,24 @@ __device__ __forceinline__ const uint16_t *sub_lcols(const SubCtx<Q> &c, int r, 
     return c.cidx + (r % kCRing) * kSW * Q * SubCfg<Q>::K + c.j * rc.CS;
 }
 // Byte offset of this lane's slot 0 of chunk rc in the tile's E; slot i is at
-// + i * 512 (an immediate offset).  Slots past the lane's piece are NOT
-// clamped: their loads read other edges (or, on the last tile's last row, the
-// allocation's kEPadEdges slack) and their values are discarded (t = 1.0, no
-// store).
+// + i * 512.  Slots past the lane's piece are NOT clamped: their loads read
+// other edges (past the tile's last edge: the buffer returns 0) and their
+// values are discarded (t = 1.0, the store dropped at kSubOOB).
 template <int Q>
 __device__ __forceinline__ uint32_t sub_eoff(const SubCtx<Q> &c, const SubChunk &rc) {
     return ((uint32_t)(rc.c0 + c.j * rc.CS) << 9) + c.lo8;
-}
-// a lane's slot i of a row chunk is at most (Q-1)*CS + K - 1 < Q*K edges past the row's end
-static_assert(4 * SubCfg<4>::K <= kEPadEdges, "E slack too small");
-template <int Q>
-__device__ __forceinline__ double *sub_es(const SubCtx<Q> &c, uint32_t off, int i) {
-    return (double *)(c.Eu + (size_t)off + (size_t)i * (kTile * sizeof(double)));
 }
 // Staging of row q's indices into the ring: issue (one index per lane, lanes <
 // the chunk size) early, commit to LDS once the wavefront has waited on its
 // other loads anyway.
 template <int Q>
 __device__ __forceinline__ int sub_stage_issue(const SubCtx<Q> &c, int q) {
-    if (q >= c.m) return 0;
-    const SubChunk rc = sub_chunk(c.row_ptr, q, c.wave, Q);
+    // always one load (an in-range edge): a conditional load into a register
+    // also written with 0 makes the compiler wait for every outstanding
+    // memory operation (this row's E_new stores) before P1's first request
+    const SubChunk rc = sub_chunk(c.row_ptr, min(q, c.m - 1), c.wave, Q);
     const int L = threadIdx.x & 63;
-    return rc.cnt > 0 ? sub_col(c, rc.c0 + min(L, rc.cnt - 1)) : 0;
+    return sub_col(c, min(max(rc.c0 + min(L, rc.cnt - 1), 0), c.row_ptr[c.m] - 1));
 }
 template <int Q>
 __device__ __forceinline__ void sub_stage_commit(const SubCtx<Q> &c, int q, int v) {
@@ -283,7 +296,7 @@ __device__ __forceinline__ bool sub_p1(const SubCtx<Q> &c, int r, const SubChunk
         for (int i = 0; i < K; ++i) {
             // iteration 0 and a fresh frame's lanes read no E_old (on a
             // streaming pass most slots hold fresh frames)
-            eo[i] = noE ? 0.0 : ld_sub_msg(sub_es(c, eoff, i));
+            eo[i] = ld_sub_msg(c.rE, noE ? kSubOOB : eoff + (uint32_t)i * (kTile * sizeof(double)));
             col[i] = lc[i];
         }
         const char *Lsrc = c.first ? c.Cu : c.Lu;  // iteration 0: M = ch (:85-90); uniform
@@ -419,7 +432,7 @@ __device__ __forceinline__ void sub_hop(const SubCtx<Q> &c, int r, const double 
 template <int Q>
 __device__ __forceinline__ void sub_order(const SubCtx<Q> &c, int r) {
     if (r > 0) {
-        const int d = c.p3dep[r * kSW + c.wave];
+        const int d = ld_table(c.p3dep, r * kSW + c.wave);
         for (int v = d & 0xff; v <= (d >> 8); ++v) wait_ge<false>(c.p3row + v, r);
     }
 }
@@ -433,11 +446,9 @@ __device__ __forceinline__ void sub_p3_body(SubCtx<Q> &c, int r, double (&t)[Sub
     // the identity column k + r is the row's last edge (an [A | I] graph):
     // the lane whose piece ends there requests its channel LLR now, ahead of
     // the chain wait (+1 % with the late S-order wait below, profiles/r5n_ab)
-    double chI = 0.0;
-    {
-        const int njI = sub_nj(c, rc);
-        if (njI > 0 && rc.c0 + c.j * rc.CS + njI == c.row_ptr[r + 1]) chI = *sub_c(c, c.k + r);
-    }
+    // (every lane requests it: a conditional load leaves the compiler's
+    // vmcnt count inexact; the 16 frames' 128 B are one line for all lanes)
+    const double chI = *sub_c(c, c.k + r);
     SUB_STAMP(q0);
     wait_flag<false>(c.flag + s, ep + kSW);
     SUB_STAMP(q1);
@@ -525,11 +536,11 @@ __device__ __forceinline__ void sub_p3_body(SubCtx<Q> &c, int r, double (&t)[Sub
             }
         }
     }
-    if (c.live) {
+    {
         const uint32_t eoff = sub_eoff(c, rc);
 #pragma unroll
-        for (int i = 0; i < K; ++i)
-            if (i < rc.CS && i < nj) st_sub_msg(sub_es(c, eoff, i), t[i]);
+        for (int i = 0; i < K; ++i)  // nj <= CS
+            st_sub_msg(c.rE, (i < nj && c.live) ? eoff + (uint32_t)i * (kTile * sizeof(double)) : kSubOOB, t[i]);
     }
     // S_col += E_new, rows ascending (a column occurs once per row: no two
     // lanes of a row share (col, frame)); the identity edge goes to `dummy`
@@ -655,6 +666,7 @@ __global__ __launch_bounds__(64 * kSW, 1) void tile_sub_kernel(DevGraph g, DevSt
     c.Lb = st.L + (size_t)tile * g.n * kTile + lo;
     c.Cb = st.ch + (size_t)tile * g.n * kTile + lo;
     c.Eu = (const char *)(st.E + (size_t)tile * g.nnz * kTile);
+    c.rE = sub_rsrc(c.Eu, (size_t)g.nnz * kTile * sizeof(double));
     c.Lu = (const char *)(st.L + (size_t)tile * g.n * kTile);
     c.Cu = (const char *)(st.ch + (size_t)tile * g.n * kTile);
     c.lo8 = (uint32_t)lo * 8u;
@@ -837,6 +849,7 @@ __global__ __launch_bounds__(64 * kSW, 1) void tile_sub_stream_kernel(
     c.Lb = st.L + (size_t)tile * g.n * kTile + lo;
     c.Cb = st.ch + (size_t)tile * g.n * kTile + lo;
     c.Eu = (const char *)(st.E + (size_t)tile * g.nnz * kTile);
+    c.rE = sub_rsrc(c.Eu, (size_t)g.nnz * kTile * sizeof(double));
     c.Lu = (const char *)(st.L + (size_t)tile * g.n * kTile);
     c.Cu = (const char *)(st.ch + (size_t)tile * g.n * kTile);
     c.lo8 = (uint32_t)lo * 8u;
