@@ -14,11 +14,25 @@
 // H_std (llr > 0)) -- and supplied heaviest first, so the frames that will
 // run long start while the slots are still being refilled.
 //
+// Round 5: equal syndrome weights (most frames have none at 2.5-3 dB) are
+// ranked by the channel reliability of the weakest identity bit whose single
+// check row has odd degree, least reliable first, on graphs where at most
+// half the rows have odd degree (wimax_2304_0.5).  There the frames that fail
+// with error-free or one-error hard decisions are exactly those (the
+// reference's check rule returns a wrong-sign extrinsic on odd-degree rows,
+// SURVEY.md §0.3, which flips a weak degree-1 bit): on 8,000 oracle-decoded
+// frames at 3 dB all 18 zero-syndrome failures rank in the first 1.3 % of the
+// zero-syndrome frames (index order: spread to 85 %), so the last failing
+// frame starts in the first ~9 % of the supply instead of at its end.
+// Codes with mostly odd rows (the r3/4 codes: there the most reliable frames
+// fail) keep index order within a syndrome weight.
+//
 // frame_score_kernel regenerates each frame with the device frame source's
 // own draws (frame_source.h: info_block / noise_pair / channel_llr, the same
 // bits gen_slots writes into the slots later) and counts its unsatisfied
-// rows; hipcub's stable radix sort orders the local frame indices by
-// descending score (ties in index order: deterministic).
+// rows (and that weakest |llr|); hipcub's stable radix sort orders the local
+// frame indices by descending key = weight << 16 | reliability rank (ties in
+// index order: deterministic).
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
 
@@ -37,6 +51,7 @@ __global__ __launch_bounds__(kScoreThreads) void frame_score_kernel(DevGraph g, 
                                                                     uint32_t *score, int *idx) {
     extern __shared__ uint32_t sh[];  // u [kw] | hard bits [nw]
     __shared__ uint32_t wsum[kScoreThreads / 64];
+    __shared__ float wmin[kScoreThreads / 64];
     const int kw = (g.k + 31) >> 5, nw = (g.n + 31) >> 5;
     uint32_t *u = sh, *hb = sh + kw;
     const double s2 = sigma * sigma;
@@ -57,6 +72,7 @@ __global__ __launch_bounds__(kScoreThreads) void frame_score_kernel(DevGraph g, 
         for (int i = threadIdx.x; i < nw; i += blockDim.x) hb[i] = 0u;
         __syncthreads();
         // codeword [u, A.u], BPSK + AWGN, LLR (channel.py:49,68-80); hard bit = llr > 0
+        float weak = INFINITY;  // min |llr| over identity bits of odd-degree rows
         for (int b = threadIdx.x; 2 * b < g.n; b += blockDim.x) {
             double gz[2];
             noise_pair(seed, F, snr_point, b, gz);
@@ -74,7 +90,10 @@ __global__ __launch_bounds__(kScoreThreads) void frame_score_kernel(DevGraph g, 
                     for (int w = 0; w < kw; ++w) acc ^= ar[w] & u[w];
                     bit = (uint32_t)__popc(acc) & 1u;
                 }
-                if (channel_llr(bit, gz[q], s2) > 0.0) hv |= 1u << q;
+                const double l = channel_llr(bit, gz[q], s2);
+                if (l > 0.0) hv |= 1u << q;
+                if (g.lpt_weak_id && j >= g.k && ((g.row_ptr[j - g.k + 1] - g.row_ptr[j - g.k]) & 1))
+                    weak = fminf(weak, (float)fabs(l));
             }
             if (hv) atomicOr(&hb[(2 * b) >> 5], hv << ((2 * b) & 31));
         }
@@ -88,14 +107,26 @@ __global__ __launch_bounds__(kScoreThreads) void frame_score_kernel(DevGraph g, 
             cnt += par & 1u;
         }
 #pragma unroll
-        for (int o = 32; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o);
-        if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = cnt;
+        for (int o = 32; o > 0; o >>= 1) {
+            cnt += __shfl_xor(cnt, o);
+            weak = fminf(weak, __shfl_xor(weak, o));
+        }
+        if ((threadIdx.x & 63) == 0) {
+            wsum[threadIdx.x >> 6] = cnt;
+            wmin[threadIdx.x >> 6] = weak;
+        }
         __syncthreads();
         if (threadIdx.x == 0) {
             uint32_t s = 0u;
+            float w = INFINITY;
 #pragma unroll
-            for (int i = 0; i < kScoreThreads / 64; ++i) s += wsum[i];
-            score[f] = s;
+            for (int i = 0; i < kScoreThreads / 64; ++i) {
+                s += wsum[i];
+                w = fminf(w, wmin[i]);
+            }
+            // |llr| >= 0: its float bits rise with it; the top 16 of 31, inverted
+            const uint32_t rel = g.lpt_weak_id ? 0xffffu - (__float_as_uint(w) >> 15) : 0u;
+            score[f] = (s << 16) | rel;
             idx[f] = f;
         }
         __syncthreads();  // u / hb / wsum are rewritten by the next frame
@@ -108,11 +139,12 @@ __global__ __launch_bounds__(kScoreThreads) void frame_score_kernel(DevGraph g, 
 size_t frame_order_temp_bytes(int total) {
     size_t bytes = 0;
     (void)hipcub::DeviceRadixSort::SortPairsDescending(nullptr, bytes, (const uint32_t *)nullptr, (uint32_t *)nullptr,
-                                                       (const int *)nullptr, (int *)nullptr, total, 0, 16);
+                                                       (const int *)nullptr, (int *)nullptr, total, 0, 32);
     return bytes;
 }
 
-// order[0..total) = the point's local frame indices, heaviest syndrome first.
+// order[0..total) = the point's local frame indices, heaviest syndrome first
+// (equal weights: least reliable odd-row identity bit first, lpt_weak_id).
 // keys: 2 x total uint32, vals: total int scratch, temp: frame_order_temp_bytes.
 hipError_t launch_frame_order(const DevGraph &g, uint64_t seed, int snr_point, double sigma, int64_t frame0,
                               int total, uint32_t *keys, int *vals, int *order, void *temp, size_t temp_bytes,
@@ -126,7 +158,7 @@ hipError_t launch_frame_order(const DevGraph &g, uint64_t seed, int snr_point, d
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     size_t bytes = temp_bytes;
-    return hipcub::DeviceRadixSort::SortPairsDescending(temp, bytes, keys, keys + total, vals, order, total, 0, 16, s);
+    return hipcub::DeviceRadixSort::SortPairsDescending(temp, bytes, keys, keys + total, vals, order, total, 0, 32, s);
 }
 
 }  // namespace ldpc

@@ -518,6 +518,11 @@ int ldpc_graph_create(int32_t m, int32_t n, const int32_t *row_ptr, const int32_
     G.std_form = std_form;
     G.ira = ira;
     G.ef = kTile;
+    {
+        int odd = 0;
+        for (int r = 0; r < m; ++r) odd += (row_ptr[r + 1] - row_ptr[r]) & 1;
+        G.lpt_weak_id = std_form && m > 0 && 2 * odd <= m;
+    }
     G.row_ptr = p;
     p += m + 1;
     G.col_idx = p;

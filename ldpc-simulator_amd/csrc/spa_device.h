@@ -44,6 +44,8 @@ struct DevGraph {
     const int *p3dep8;         // [m][16] the same over each row's A edges (tile8.hip: identity excluded)
     int ef;                    // frames per E block (64, or 8 for tile8.hip's graphs): e_base
     int t8pair;                // tile8.hip runs its pair form (two rows per wavefront) on this graph
+    int lpt_weak_id;           // frame_order.hip: rank equal syndromes by the weakest identity bit of an
+                               // odd-degree row (set when at most half the rows have odd degree)
 };
 
 // E layout inside a tile: the 64 frames in blocks of g.ef, each block

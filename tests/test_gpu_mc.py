@@ -329,15 +329,23 @@ def test_supply_order_keeps_counters(gpu_available, monkeypatch, code, cap, fram
                                             ("wimax_576_0.5", 1.0, 1000)])
 def test_frame_order_matches_host_ranking(gpu_available, code, snr, count):
     """frame_order.hip's supply order == the stable descending ranking by the
-    syndrome weight of H_std (llr > 0), recomputed on the host from the
-    oracle's restatement of the device frame source (oracle/channel_oracle.c)."""
-    H = hstd_for(code)
+    syndrome weight of H_std (llr > 0) and, for equal weights on graphs with
+    at most half the rows of odd degree, the least reliable identity bit of an
+    odd-degree row first -- recomputed on the host from the oracle's
+    restatement of the device frame source (oracle/channel_oracle.c)."""
+    H = hstd_for(code).tocsr()
+    m, n = H.shape
     sig = oracle.sigma_for_snr(snr)
     frame0 = 123457
     order = _decoder(code, 64).frame_order(SEED, 2, sig, frame0, count)
     _, _, llr = oracle.generate_frames(H, SEED, 2, sig, frame0, count)
     hard = (llr > 0.0).astype(np.int64)
-    w = ((H @ hard.T) % 2).sum(axis=0)
-    want = np.argsort(-w, kind="stable")
+    w = np.asarray(((H @ hard.T) % 2).sum(axis=0)).ravel().astype(np.uint64)
+    odd = (np.diff(H.indptr) % 2) == 1
+    key = w << np.uint64(16)
+    if 2 * odd.sum() <= m:
+        weak = np.abs(llr[:, n - m:][:, odd]).astype(np.float32).min(axis=1)
+        key |= np.uint64(0xFFFF) - (weak.view(np.uint32) >> 15).astype(np.uint64)
+    want = np.argsort(-key.astype(np.int64), kind="stable")
     np.testing.assert_array_equal(order, want)
     assert w[order[0]] >= w[order[-1]]
