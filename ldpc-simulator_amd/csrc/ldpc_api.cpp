@@ -963,7 +963,19 @@ int mc_stream_point(ldpc_decoder *d, uint64_t seed, int p, double sigma, int64_t
     const DevGraph &G = d->g->dg;
     const int ntiles = (int)std::min<int64_t>(d->cap_tiles, (total + kTile - 1) / kTile);
     const int *order = nullptr;  // supply order (null: frame index order)
-    if (lpt_enabled() && total > 1 && total <= INT32_MAX && G.std_form && G.a_packed && G.m <= 65535) {
+    // only when frames wait for a slot: with every frame running from the
+    // start the order cannot change when any of them runs.  The split path
+    // runs every slot each launch; a tile streaming kernel keeps one
+    // workgroup per CU resident (its other workgroups start as those finish)
+    int64_t running = (int64_t)ntiles * kTile;
+    if (!split && ldpc::use_tile_stream(G)) {
+        int dev = 0, cus = 256;
+        if (hipGetDevice(&dev) == hipSuccess)
+            (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+        const int fpw = G.ef == 8 ? 8 : ldpc::sub_frames(G) == 16 ? 16 : kTile;
+        running = std::min<int64_t>(running, (int64_t)cus * fpw);
+    }
+    if (lpt_enabled() && total > running && total <= INT32_MAX && G.std_form && G.a_packed && G.m <= 65535) {
         if (int rc = ensure_order(d, total)) return rc;
         HIP_TRY(timed(d, LDPC_K_GEN, s, [&] {
             return ldpc::launch_frame_order(G, seed, p, sigma, frame0, (int)total, d->ord_keys, d->ord_vals, d->ord,
