@@ -857,7 +857,9 @@ bool use_cn_row(const DevGraph &g) {
 // few-tile streaming tail, where one 16-wavefront workgroup per CU is all
 // that fits, 1.5 % slower (profiles/r2aw_cn_row16).  LDPC_CN_ROW16 (read per
 // call): 0 = never, 1 = at any tile count, N > 1 = from N tiles, unset = from
-// 64 tiles.
+// 64 tiles -- but cn_sub_kernel takes the 2304 codes up to 128 tiles first
+// (use_cn_sub; round 5: equal on a 128-tile split chunk, 8 % faster in the
+// 3 dB streaming tail, profiles/r5_ab/r5ad_ab), so this runs above 128.
 constexpr int kRow16W = 16, kRow16K = 40;
 bool use_cn_row16(const DevGraph &g, int ntiles) {
     if (use_cn_row(g) || g.max_row_deg > kRow16W * kRow16K) return false;

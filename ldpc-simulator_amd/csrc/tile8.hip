@@ -208,10 +208,10 @@ __device__ __forceinline__ uint32_t t8_es(const T8Ctx<K> &c, uint32_t off, int i
 // lanes < the chunk size), commit once the wavefront has waited anyway.
 template <int K>
 __device__ __forceinline__ int t8_stage_issue(const T8Ctx<K> &c, int q) {
-    if (q >= c.m) return 0;
-    const T8Chunk rc = t8_chunk(c.row_ptr, q, c.wave);
+    // always one load of an in-range edge (see t8_prefetch)
+    const T8Chunk rc = t8_chunk(c.row_ptr, min(q, c.m - 1), c.wave);
     const int L = threadIdx.x & 63;
-    return rc.cnt > 0 ? c.col_idx[rc.c0 + min(L, rc.cnt - 1)] : 0;
+    return c.col_idx[min(max(rc.c0 + min(L, rc.cnt - 1), 0), c.nnz - 1)];
 }
 template <int K>
 __device__ __forceinline__ void t8_stage_commit(const T8Ctx<K> &c, int q, int v) {
@@ -236,18 +236,21 @@ struct T8Pre {
 };
 // (iteration 0 and a fresh streaming frame's lanes form M = L - 0.0 == L and
 // read no E_old: exec-masked)
+// Every load is issued unconditionally, masked ones at kOOB (the buffer
+// returns 0 without a memory request): with loads under branches the
+// compiler's vmcnt counts were conservative and P1 waited for the previous
+// row's E_new stores before its first request (tile_sub.hip, round 5).
 template <int K>
 __device__ __forceinline__ void t8_prefetch(const T8Ctx<K> &c, int r, T8Pre<K> &p) {
     const T8Chunk rc = t8_chunk(c.row_ptr, r, c.wave);
-    if (rc.cnt > 0) {
-        const uint32_t eoff = t8_eoff(c, rc);
+    const bool noE = c.first || c.fresh;
+    const uint32_t eoff = t8_eoff(c, rc);
 #pragma unroll
-        for (int i = 0; i < K; ++i) p.eo[i] = (c.first || c.fresh) ? 0.0 : t8_ld<kNT>(c.rE, t8_es(c, eoff, i));
-    }
-    if (c.wave == c.idwave && rc.deg > 0) {  // identity edge (a fresh streaming frame has L = ch: gen_slots)
-        p.lid = t8_ld(c.first ? c.rC : c.rL, ((uint32_t)(c.k + r) << 9) + c.lo8);
-        p.eid = (c.first || c.fresh) ? 0.0 : t8_ld<kNT>(c.rE, ((uint32_t)(rc.beg + rc.deg - 1) << 6) + c.eo8);
-    }
+    for (int i = 0; i < K; ++i) p.eo[i] = t8_ld<kNT>(c.rE, (rc.cnt > 0 && !noE) ? t8_es(c, eoff, i) : kOOB);
+    // identity edge (a fresh streaming frame has L = ch: gen_slots)
+    const bool id = c.wave == c.idwave && rc.deg > 0;
+    p.lid = t8_ld(c.first ? c.rC : c.rL, id ? ((uint32_t)(c.k + r) << 9) + c.lo8 : kOOB);
+    p.eid = t8_ld<kNT>(c.rE, (id && !noE) ? ((uint32_t)(rc.beg + rc.deg - 1) << 6) + c.eo8 : kOOB);
 }
 
 // P1: t = tanh((L[col] - E_old)/2) for this lane's slots, columns into col[];
@@ -295,12 +298,10 @@ __device__ __forceinline__ bool t8_p1(const T8Ctx<K> &c, int r, const T8Pre<K> &
     bool tiny = false;
     const int sv = t8_stage_issue(c, r + 1);
     const T8Chunk rc = t8_chunk(c.row_ptr, r, c.wave);
-    if (rc.cnt > 0) {
-        t8_p1_slots<K, LA>(c, r, rc, pre, t, tiny, rc.CS < K);
-    } else {
-#pragma unroll
-        for (int i = 0; i < K; ++i) t[i] = 1.0;
-    }
+    // no branch on rc.cnt (its loads stay unconditional: t8_prefetch); an
+    // empty chunk has nj = 0, so every slot ends as 1.0 (the staged indices
+    // are valid columns)
+    t8_p1_slots<K, LA>(c, r, rc, pre, t, tiny, rc.CS < K);
     if (c.wave == c.idwave && rc.deg > 0) {  // the identity edge: t_id, published for every P3 of row r
         const double M = c.fresh ? pre.lid : pre.lid - pre.eid;
         const double tv = tanh_half_clipped(M, c.ttab);
@@ -400,8 +401,7 @@ __device__ __forceinline__ void t8_p3(T8Ctx<K> &c, int r, double (&t)[K]) {
     const int s = r & (kSR8 - 1);
     const int ep = ((c.ep0 + r) & 0x3ffffff) * 32;
     const bool idw = c.wave == c.idwave;  // holds the identity edge
-    double chI = 0.0;
-    if (idw) chI = t8_ld(c.rC, ((uint32_t)(c.k + r) << 9) + c.lo8);  // for L = ch + (0 + E)
+    const double chI = t8_ld(c.rC, idw ? ((uint32_t)(c.k + r) << 9) + c.lo8 : kOOB);  // for L = ch + (0 + E)
     int col[K];  // staged indices (ring row r is live until body(r + D - 1) ends)
     {
         const uint16_t *lc = t8_lcols(c, r, rc);
@@ -510,19 +510,18 @@ __device__ __forceinline__ void t8_p3(T8Ctx<K> &c, int r, double (&t)[K]) {
             EI = 2.0 * atanh_f(clip_cl(q), c.ltab, c.ac);
         }
     }
-    if (rc.cnt > 0) {  // slots past the piece (and frames that stopped) store out of range: dropped
+    {  // slots past the piece (and frames that stopped) store out of range: dropped (no branch)
         const uint32_t eoff = t8_eoff(c, rc);
 #pragma unroll
         for (int i = 0; i < K; ++i) t8_st<kEStAux>(c.rE, (i < nj && c.live) ? t8_es(c, eoff, i) : kOOB, t[i]);
-    }
-    if (c.live) {
-        if (idw && c.j == 0) t8_st<kEStAux>(c.rE, ((uint32_t)(rc.beg + rc.deg - 1) << 6) + c.eo8, EI);
+        t8_st<kEStAux>(c.rE, (c.live && idw && c.j == 0) ? ((uint32_t)(rc.beg + rc.deg - 1) << 6) + c.eo8 : kOOB,
+                       EI);
     }
     // S order: row r-1's P3 by the overlapping wavefronts
     T8_STAMP(q2);
     T8_ADD(c, 3, q1, q2);
     if (r > 0) {
-        const int d = c.p3dep[r * kW8 + c.wave];
+        const int d = ld_table(c.p3dep, r * kW8 + c.wave);
         for (int v = d & 0xff; v <= (d >> 8); ++v) wait_ge<false>(c.p3row + v, r);
     }
     T8_STAMP(q3);
@@ -537,10 +536,11 @@ __device__ __forceinline__ void t8_p3(T8Ctx<K> &c, int r, double (&t)[K]) {
         for (int i = 0; i < K; ++i)  // one ds_add_f64 per slot; past the piece: `dummy`
             __hip_atomic_fetch_add(sp[i], t[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
-    if (idw && c.j == 0) {  // identity column: L = ch + (0 + E) (:173-185)
+    {  // identity column: L = ch + (0 + E) (:173-185)
+        const bool own = idw && c.j == 0;
         const double Lj = chI + (0.0 + EI);
-        if (c.live) t8_st(c.rL, ((uint32_t)(c.k + r) << 9) + c.lo8, Lj);
-        if (!(Lj < 0.0)) atomicOr(c.ib + (r >> 5) * kF8, 1u << (r & 31));
+        t8_st(c.rL, (own && c.live) ? ((uint32_t)(c.k + r) << 9) + c.lo8 : kOOB, Lj);
+        if (own && !(Lj < 0.0)) atomicOr(c.ib + (r >> 5) * kF8, 1u << (r & 31));
     }
     lds_release();  // this row's S additions before the count
     if ((threadIdx.x & 63) == 0) lds_st(c.p3row + c.wave, r + 1);

@@ -51,3 +51,18 @@ def model(o, slots=4096, ctail=0.54):
 
 for name, o in (("device order", order), ("index order", np.arange(N)), ("by iterations", np.argsort(-its, kind="stable"))):
     print("%-14s supply %5.1f passes, tail %5.1f, total %6.1f" % ((name,) + model(o)))
+
+# the failing frames the order starts late: what the receiver saw
+Hc = H.tocsr()
+m, n = Hc.shape
+k = n - m
+odd = (np.diff(Hc.indptr) % 2) == 1
+late = np.where(fail & (pos > 0.1 * N))[0]
+for f in late[:12]:
+    _, l1 = dec.generate(seed, point, sig, frame0 + int(f), 1)
+    l1 = l1[0]
+    hard = (l1 > 0).astype(np.int64)
+    syn = int(((Hc @ hard) % 2).sum())
+    a = np.abs(l1)
+    print(f"late failing frame {f}: pos {pos[f] / N:.3f} iters {its[f]} syn {syn} minI_odd {a[k:][odd].min():.3f} "
+          f"minI_even {a[k:][~odd].min():.3f} minA {a[:k].min():.4f} neg-bits {int((l1 < 0).sum())}")
