@@ -1224,29 +1224,44 @@ int phys_decode_lds(const ldpc_graph *g, int32_t batch, const double *llr, int32
 
 // Decode the frames bound in d->st (channel LLRs in d->ch) on graph P with the
 // HBM-resident tile kernels: up to max_iter CN+VN sweeps, then a syndrome-only
-// sweep.  The host reads the running-tile count after VN(it) for it < 4 and
-// every 4th iteration after, and stops issuing sweeps once it is zero.
-int phys_tile_decode(ldpc_decoder *d, const DevGraph &P, int max_iter, bool from_ch, hipStream_t s) {
-    if (d->pactive_cap < max_iter) {
+// sweep.  The host reads the running-tile and running-frame counts after
+// VN(it) for it < 4 and every 4th iteration after, and stops issuing sweeps
+// once they are zero.  With ctr (a Monte-Carlo run: only the counters leave
+// the device) the running frames are compacted into the first tiles once at
+// most a quarter of the launched slots hold them, the finished frames counted
+// into ctr first (phys_tile.hip).
+int phys_tile_decode(ldpc_decoder *d, const DevGraph &P, int max_iter, bool from_ch, hipStream_t s,
+                     unsigned long long *ctr = nullptr) {
+    if (d->pactive_cap < 2 * max_iter) {
         (void)hipFree(d->pactive);
         d->pactive = nullptr;
         d->pactive_cap = 0;
-        if (int rc = dev_alloc(&d->pactive, (size_t)max_iter)) return rc;
-        d->pactive_cap = max_iter;
+        if (int rc = dev_alloc(&d->pactive, 2 * (size_t)max_iter)) return rc;
+        d->pactive_cap = 2 * max_iter;
     }
-    const DevState st = d->st;
+    DevState st = d->st;  // st.ntiles shrinks with each compaction
     const PhysTile pt = phys_tile(d);
-    HIP_TRY(hipMemsetAsync(d->pactive, 0, sizeof(int) * max_iter, s));
+    const int cap = d->cap_tiles * kTile;
+    HIP_TRY(hipMemsetAsync(d->pactive, 0, sizeof(int) * 2 * max_iter, s));
     HIP_TRY(ldpc::launch_phys_tile_init(P, st, pt, from_ch, s));
     for (int it = 0; it < max_iter; ++it) {
         HIP_TRY(timed(d, LDPC_K_PHYS_CN, s, [&] { return ldpc::launch_phys_tile_cn(P, st, pt, it, false, s); }));
         HIP_TRY(timed(d, LDPC_K_PHYS_VN, s,
-                      [&] { return ldpc::launch_phys_tile_vn(P, st, pt, it, d->pactive, s); }));
+                      [&] { return ldpc::launch_phys_tile_vn(P, st, pt, it, d->pactive, max_iter, s); }));
         if (it + 1 < max_iter && (it < 4 || (it + 1) % 4 == 0)) {
-            int running = 0;
-            HIP_TRY(hipMemcpyAsync(&running, d->pactive + it, sizeof(int), hipMemcpyDeviceToHost, s));
+            int running[2] = {0, 0};  // tiles, frames
+            HIP_TRY(hipMemcpyAsync(&running[0], d->pactive + it, sizeof(int), hipMemcpyDeviceToHost, s));
+            HIP_TRY(hipMemcpyAsync(&running[1], d->pactive + max_iter + it, sizeof(int), hipMemcpyDeviceToHost, s));
             HIP_TRY(hipStreamSynchronize(s));
-            if (running == 0) break;  // every frame has stopped (converged; final() leaves them alone)
+            if (running[0] == 0) break;  // every frame has stopped (converged; final() leaves them alone)
+            const int nt = (running[1] + kTile - 1) / kTile;
+            // (a quarter: half measured the same, profiles/r5_ab/r5am_ab)
+            if (ctr && nt < st.ntiles && 4 * (int64_t)running[1] <= (int64_t)st.ntiles * kTile) {
+                if (!d->cpairs && dev_alloc(&d->cpairs, 1 + 2 * (size_t)cap)) return LDPC_ENOMEM;
+                HIP_TRY(timed(d, LDPC_K_COUNT, s, [&] { return ldpc::launch_phys_tile_count(P, st, pt, ctr, s); }));
+                HIP_TRY(ldpc::launch_phys_compact(P, st, pt, nt, cap, d->cpairs, s));
+                st.ntiles = nt;
+            }
         }
     }
     HIP_TRY(ldpc::launch_phys_tile_cn(P, st, pt, max_iter, true, s));
@@ -1368,7 +1383,7 @@ int ldpc_phys_mc_run(ldpc_decoder *d, const ldpc_graph *gp, uint64_t seed, int32
                                              nullptr, st.ubits, ctr, std::min(phys_grid(P), cnt), s);
                 }));
             } else {
-                if (int rc = phys_tile_decode(d, P, max_iter, false, s)) return rc;
+                if (int rc = phys_tile_decode(d, P, max_iter, false, s, ctr)) return rc;
                 HIP_TRY(timed(d, LDPC_K_COUNT, s,
                               [&] { return ldpc::launch_phys_tile_count(P, st, phys_tile(d), ctr, s); }));
             }

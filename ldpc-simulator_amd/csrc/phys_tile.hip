@@ -19,7 +19,14 @@
 //                 A frame whose syndrome was zero stops here, converged at
 //                 the previous iteration (exactly the LDS kernel's exit).
 // After the last iteration a syndrome-only CN sweep and phys_tile_final give
-// the frames that converge on it.  Each (tile, row block) and (tile, column
+// the frames that converge on it.
+// Monte-Carlo runs (counters only) compact: once at most a quarter of the
+// launched slots still run, the finished frames are counted and the running
+// ones move into the first tiles (phys_compact_*), so the last sweeps launch
+// those tiles only -- at 1 dB on the DVB-S2 profile the fourth CN sweep ran
+// for ~5 % of the frames, scattered over every tile, at the cost of a full
+// sweep (profiles/r5s_c5).  done[]: 0 running, 1 finished (to be counted),
+// 2 counted, moved away, or no frame.  Each (tile, row block) and (tile, column
 // block) is placed XCD-aware like cn_kernel.
 // Frames come from frame_kernels.hip (directly as fp32 Lambda/L for IRA
 // codes, else as fp64 ch converted by phys_tile_init).
@@ -71,7 +78,7 @@ __global__ void phys_tile_init_kernel(DevGraph g, DevState st, PhysTile pt, int 
     if (i < (size_t)st.ntiles * kTile) {
         const int f = (int)i;
         const bool valid = f < st.count;
-        st.done[f] = valid ? 0 : 1;
+        st.done[f] = valid ? 0 : 2;  // 2: no frame (never counted)
         st.conv[f] = -1;
         st.status[f] = 1;
         st.iters[f] = 0;
@@ -165,7 +172,8 @@ __global__ __launch_bounds__(256) void phys_cn_tile_kernel(DevGraph g, DevState 
 
 __global__ __launch_bounds__(256) void phys_vn_tile_kernel(DevGraph g, DevState st, PhysTile pt, int it,
                                                            int per_tile, int items, const int *__restrict__ csc_ptr,
-                                                           const int *__restrict__ csc_edge, int *active_count) {
+                                                           const int *__restrict__ csc_edge, int *active_count,
+                                                           int max_iter) {
     const int lane = threadIdx.x & 63;
     const int wave = uniform(threadIdx.x >> 6);
     for (int item = blockIdx.x; item < items; item += gridDim.x) {
@@ -202,7 +210,10 @@ __global__ __launch_bounds__(256) void phys_vn_tile_kernel(DevGraph g, DevState 
         const unsigned long long any = __ballot(upd);
         if (lane == 0) {
             st.tile_active[tile] = any != 0ull ? 1 : 0;
-            if (any) atomicAdd(&active_count[it], 1);  // host polls: 0 -> every frame has stopped
+            if (any) {
+                atomicAdd(&active_count[it], 1);  // host polls: 0 -> every frame has stopped
+                atomicAdd(&active_count[max_iter + it], (int)__popcll(any));  // running frames (compaction)
+            }
         }
     }
     }
@@ -238,7 +249,7 @@ __global__ __launch_bounds__(64) void phys_tile_count_kernel(DevGraph g, DevStat
     const int tile = blockIdx.x / per_tile, part = blockIdx.x % per_tile;
     const int lane = threadIdx.x;
     const int f = tile * kTile + lane;
-    const bool valid = f < st.count;
+    const bool valid = st.done[f] == 1;  // finished and not counted yet (phys_tile_init, phys_compact)
     const bool failed = valid && st.status[f] != 0;
     unsigned long long err = 0;
     if (__ballot(failed) != 0ull) {  // BER counts failed frames only (main.py:130-138)
@@ -263,6 +274,58 @@ __global__ __launch_bounds__(64) void phys_tile_count_kernel(DevGraph g, DevStat
         const unsigned long long s = wave_sum(v[i]);
         if (lane == 0 && s) atomicAdd(&ctr[i], s);
     }
+}
+
+// Compaction (Monte-Carlo runs): after the finished frames were counted,
+// mark them counted; then move each running frame of the plan (spa_kernels
+// compact plan: sources = running slots in tiles >= nt, destinations =
+// finished slots below) -- its lanes of E32, L32, Lambda and the u bits --
+// and reset the destination's per-frame state.  Sources and destinations are
+// disjoint, so the moves need no ordering.
+__global__ void phys_mark_counted_kernel(DevState st) {
+    const int f = blockIdx.x * blockDim.x + threadIdx.x;
+    if (f < st.ntiles * kTile && st.done[f] == 1) st.done[f] = 2;
+}
+__global__ void phys_compact_move_kernel(DevGraph g, DevState st, PhysTile pt, int cap, const int *pairs) {
+    const int P = pairs[0];
+    const int kw = (g.k + 31) >> 5;
+    const int64_t items = (int64_t)g.nnz + 2 * (int64_t)g.n + kw;
+    const int64_t total = (int64_t)P * items;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+        const int p = (int)(i % P);  // pair-fastest: neighbouring lanes of one item
+        int64_t it = i / P;
+        const int src = pairs[1 + p], dst = pairs[1 + cap + p];
+        const size_t sT = src >> 6, sl = src & 63, dT = dst >> 6, dl = dst & 63;
+        if (it < g.nnz) {
+            pt.E[(dT * g.nnz + it) * kTile + dl] = pt.E[(sT * g.nnz + it) * kTile + sl];
+            continue;
+        }
+        it -= g.nnz;
+        if (it < g.n) {
+            pt.L[(dT * g.n + it) * kTile + dl] = pt.L[(sT * g.n + it) * kTile + sl];
+            continue;
+        }
+        it -= g.n;
+        if (it < g.n) {
+            pt.Lam[(dT * g.n + it) * kTile + dl] = pt.Lam[(sT * g.n + it) * kTile + sl];
+            continue;
+        }
+        it -= g.n;
+        st.ubits[(dT * kw + it) * kTile + dl] = st.ubits[(sT * kw + it) * kTile + sl];
+    }
+}
+__global__ void phys_compact_flags_kernel(DevState st, PhysTile pt, int cap, const int *pairs) {
+    const int p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= pairs[0]) return;
+    const int src = pairs[1 + p], dst = pairs[1 + cap + p];
+    st.done[dst] = 0;
+    st.conv[dst] = -1;
+    st.status[dst] = 1;
+    st.iters[dst] = 0;
+    pt.bad[dst] = 0;
+    pt.bad[pt.cap + dst] = 0;
+    st.tile_active[dst >> 6] = 1;
+    st.done[src] = 2;  // moved: nothing to count here
 }
 
 inline unsigned grid_for(size_t total, int block) { return (unsigned)((total + block - 1) / block); }
@@ -296,11 +359,11 @@ hipError_t launch_phys_tile_cn(const DevGraph &g, const DevState &st, const Phys
 }
 
 hipError_t launch_phys_tile_vn(const DevGraph &g, const DevState &st, const PhysTile &pt, int it, int *active_count,
-                               hipStream_t s) {
+                               int max_iter, hipStream_t s) {
     const int per_tile = (g.n + 4 * kColsPerWave - 1) / (4 * kColsPerWave);
     const int items = (int)xcd_items(st.ntiles, per_tile);
     phys_vn_tile_kernel<<<stride_grid(items), 256, 0, s>>>(g, st, pt, it, per_tile, items, g.csc_ptr, g.csc_edge,
-                                                           active_count);
+                                                           active_count, max_iter);
     return hipGetLastError();
 }
 
@@ -314,6 +377,15 @@ hipError_t launch_phys_tile_out(const DevGraph &g, const DevState &st, const Phy
                                 hipStream_t s) {
     const size_t total = (size_t)st.count * g.n;
     if (total && (z || post)) phys_tile_out_kernel<<<grid_for(total, 256), 256, 0, s>>>(g, st, pt, z, post);
+    return hipGetLastError();
+}
+
+hipError_t launch_phys_compact(const DevGraph &g, const DevState &st, const PhysTile &pt, int nt, int cap, int *pairs,
+                               hipStream_t s) {
+    phys_mark_counted_kernel<<<grid_for((size_t)st.ntiles * kTile, 256), 256, 0, s>>>(st);
+    if (hipError_t e = launch_compact_plan(st, nt, cap, pairs, s)) return e;
+    phys_compact_move_kernel<<<2048, 256, 0, s>>>(g, st, pt, cap, pairs);
+    phys_compact_flags_kernel<<<grid_for((size_t)cap, 256), 256, 0, s>>>(st, pt, cap, pairs);
     return hipGetLastError();
 }
 

@@ -180,6 +180,8 @@ hipError_t launch_refill(const DevGraph &g, const DevState &st, uint64_t seed, i
 // streaming tail: move the frames running in tiles >= nt into finished slots
 // of tiles < nt (pairs: 1 + 2 cap ints of scratch)
 hipError_t launch_compact(const DevGraph &g, const DevState &st, int nt, int cap, int *pairs, hipStream_t s);
+// the plan alone (phys_tile.hip's compaction moves its own arrays)
+hipError_t launch_compact_plan(const DevState &st, int nt, int cap, int *pairs, hipStream_t s);
 hipError_t launch_finalize(const DevGraph &g, const DevState &st, uint8_t *z, double *post,
                            hipStream_t s);
 hipError_t launch_export_msgs(const DevGraph &g, const DevState &st, double *out, hipStream_t s);
@@ -213,6 +215,9 @@ hipError_t launch_phys_tile_cn(const DevGraph &g, const DevState &st, const Phys
                                hipStream_t s);
 // active_count[it] += tiles that still have a running frame after VN(it)
 hipError_t launch_phys_tile_vn(const DevGraph &g, const DevState &st, const PhysTile &pt, int it, int *active_count,
+                               int max_iter, hipStream_t s);  // active_count [2 max_iter]: tiles, then frames
+// Monte-Carlo compaction of the running frames into tiles < nt (the finished ones counted first)
+hipError_t launch_phys_compact(const DevGraph &g, const DevState &st, const PhysTile &pt, int nt, int cap, int *pairs,
                                hipStream_t s);
 hipError_t launch_phys_tile_final(const DevGraph &g, const DevState &st, const PhysTile &pt, int max_iter,
                                   hipStream_t s);

@@ -1081,6 +1081,11 @@ __global__ void tile_active_kernel(DevState st) {  // after a compaction: which 
     if (lane == 0) st.tile_active[tile] = busy != 0ull ? 1 : 0;
 }
 
+hipError_t launch_compact_plan(const DevState &st, int nt, int cap, int *pairs, hipStream_t s) {
+    compact_plan_kernel<<<1, 1024, 0, s>>>(st, nt, cap, pairs);
+    return hipGetLastError();
+}
+
 hipError_t launch_compact(const DevGraph &g, const DevState &st, int nt, int cap, int *pairs, hipStream_t s) {
     compact_plan_kernel<<<1, 1024, 0, s>>>(st, nt, cap, pairs);
     compact_move_kernel<<<2048, 256, 0, s>>>(g, st, cap, pairs);

@@ -89,8 +89,15 @@ def test_phys_mc_hbm_counters_equal_lds(gpu_available):
     gp = _graph(edd.physical_matrix())
     sig = [mc.sigma_for_snr(s) for s in (-3.0, -2.5, 0.0)]
     a = dec.phys_mc_run(gp, SEED, sig, 2000, 64, 50)
+    dec.profile(True)
     b = dec.phys_mc_run(gp, SEED, sig, 2000, 64, 50, hbm=True)
+    p = dec.profile_read()
+    dec.profile(False)
     np.testing.assert_array_equal(a, b)
+    # the HBM path compacted its running frames (round 5: the finished frames
+    # are counted before the move, so more count launches than chunks)
+    chunks = 3 * 2
+    assert p["count"][1] > chunks, p["count"]
 
 
 @pytest.mark.gpu
