@@ -191,13 +191,16 @@ __global__ __launch_bounds__(256) void phys_vn_tile_kernel(DevGraph g, DevState 
     if (__ballot(upd) != 0ull) {
         const int j0 = (part * 4 + wave) * kColsPerWave;
         const int j1 = min(g.n, j0 + kColsPerWave);
+        uint32_t hb = 0u;  // this lane's hard decisions of the 8 columns (early syndrome)
         for (int j = j0; j < j1; ++j) {
             if (upd) {  // lane-masked: converged / finished frames move no data
                 float s = Lamt[j * kTile];
                 for (int p = csc_ptr[j]; p < csc_ptr[j + 1]; ++p) s += ld_e32(&Et[csc_edge[p] * kTile]);
                 Lt[j * kTile] = s;
+                hb |= (s < 0.0f ? 1u : 0u) << (j - j0);
             }
         }
+        if (j0 < g.n) pt.zb[((size_t)tile * ((g.n + 7) >> 3) + (j0 >> 3)) * kTile + lane] = (uint8_t)hb;
     }
     if (part == 0 && wave == 0) {
         if (conv_now) {  // syndrome of iteration it-1 was zero
@@ -216,6 +219,65 @@ __global__ __launch_bounds__(256) void phys_vn_tile_kernel(DevGraph g, DevState 
             }
         }
     }
+    }
+}
+
+// Early syndrome: the row parities of the hard decisions VN(it) just wrote
+// (pt.zb: one byte per 8 columns, kColsPerWave == 8), one wavefront per
+// (tile, 4 rows) like phys_cn_tile, into bad[(it+1)&1] -- the flag CN(it+1)
+// would set from the same posterior.  Then phys_tile_exit stops the frames
+// whose flag stayed 0: converged at iteration it (the exit VN(it+1) would have
+// taken, one CN sweep earlier).  Only the running frames' bytes are current.
+static_assert(kColsPerWave == 8, "one hard-decision byte per VN wavefront");
+__global__ __launch_bounds__(256) void phys_tile_syn_kernel(DevGraph g, DevState st, PhysTile pt, int it,
+                                                            int per_tile, int items, const int *__restrict__ row_ptr,
+                                                            const int *__restrict__ col_idx) {
+    const int lane = threadIdx.x & 63;
+    const int wave = uniform(threadIdx.x >> 6);
+    const size_t nb = (size_t)(g.n + 7) >> 3;
+    for (int item = blockIdx.x; item < items; item += gridDim.x) {
+        int tile, part;
+        xcd_item(item, per_tile, tile, part);
+        if (tile >= st.ntiles || !st.tile_active[tile]) continue;
+        const int f = tile * kTile + lane;
+        const bool live = st.done[f] == 0;
+        if (__ballot(live) == 0ull) continue;
+        const uint8_t *zt = pt.zb + (size_t)tile * nb * kTile + lane;
+        uint32_t bad = 0u;
+        const int r0 = (part * 4 + wave) * kRowsPerWave;
+        for (int rr = 0; rr < kRowsPerWave; ++rr) {
+            const int r = r0 + rr;
+            if (r >= g.m) break;
+            uint32_t hp = 0u;
+            for (int e = row_ptr[r]; e < row_ptr[r + 1]; ++e) {
+                const int c = col_idx[e];
+                hp ^= ((uint32_t)zt[(size_t)(c >> 3) * kTile] >> (c & 7)) & 1u;
+            }
+            bad |= hp;
+        }
+        if (live && bad) pt.bad[((it + 1) & 1) * pt.cap + f] = 1;
+    }
+}
+__global__ __launch_bounds__(64) void phys_tile_exit_kernel(DevState st, PhysTile pt, int it, int *active_count,
+                                                            int max_iter) {
+    const int tile = blockIdx.x;
+    const int lane = threadIdx.x;
+    const int f = tile * kTile + lane;
+    const bool live = st.tile_active[tile] && st.done[f] == 0;
+    const bool conv_now = live && pt.bad[((it + 1) & 1) * pt.cap + f] == 0;
+    if (conv_now) {  // the syndrome of iteration it is zero
+        st.done[f] = 1;
+        st.conv[f] = it;
+        st.status[f] = 0;
+        st.iters[f] = it + 1;
+    }
+    const unsigned long long still = __ballot(live && !conv_now);
+    if (lane == 0) {
+        if (st.tile_active[tile]) st.tile_active[tile] = still != 0ull ? 1 : 0;
+        if (still) {
+            atomicAdd(&active_count[it], 1);
+            atomicAdd(&active_count[max_iter + it], (int)__popcll(still));
+        }
     }
 }
 
@@ -377,6 +439,17 @@ hipError_t launch_phys_tile_out(const DevGraph &g, const DevState &st, const Phy
                                 hipStream_t s) {
     const size_t total = (size_t)st.count * g.n;
     if (total && (z || post)) phys_tile_out_kernel<<<grid_for(total, 256), 256, 0, s>>>(g, st, pt, z, post);
+    return hipGetLastError();
+}
+
+hipError_t launch_phys_tile_early_exit(const DevGraph &g, const DevState &st, const PhysTile &pt, int it,
+                                       int *active_count, int max_iter, hipStream_t s) {
+    const int per_tile = (g.m + 4 * kRowsPerWave - 1) / (4 * kRowsPerWave);
+    const int items = (int)xcd_items(st.ntiles, per_tile);
+    phys_tile_syn_kernel<<<stride_grid(items), 256, 0, s>>>(g, st, pt, it, per_tile, items, g.row_ptr, g.col_idx);
+    if (hipError_t e = hipMemsetAsync(active_count + it, 0, sizeof(int), s)) return e;
+    if (hipError_t e = hipMemsetAsync(active_count + max_iter + it, 0, sizeof(int), s)) return e;
+    phys_tile_exit_kernel<<<st.ntiles, kTile, 0, s>>>(st, pt, it, active_count, max_iter);
     return hipGetLastError();
 }
 

@@ -83,6 +83,7 @@ struct PhysTile {
     uint32_t *pbits;   // [tile][m/32][64] IRA: in-word prefix XOR of s = H_info u (generator scratch)
     uint32_t *wpar;    // [tile][m/1024][64] IRA: bit w = parity of s words before w
     int cap;           // frames of capacity (stride of bad)
+    uint8_t *zb;       // [tile][ceil(n/8)][64] hard-decision bits of the last VN sweep (bit j&7 of byte j>>3: L < 0)
 };
 
 // --- launchers (spa_kernels.hip); all asynchronous on `s` ---
@@ -216,6 +217,11 @@ hipError_t launch_phys_tile_cn(const DevGraph &g, const DevState &st, const Phys
 // active_count[it] += tiles that still have a running frame after VN(it)
 hipError_t launch_phys_tile_vn(const DevGraph &g, const DevState &st, const PhysTile &pt, int it, int *active_count,
                                int max_iter, hipStream_t s);  // active_count [2 max_iter]: tiles, then frames
+// Syndrome of the posterior of iteration it right after VN(it), from the VN's
+// hard-decision bytes, and the exits it implies (conv = it): the frames that
+// converge there skip CN(it+1); active_count[it] / [max_iter + it] recounted
+hipError_t launch_phys_tile_early_exit(const DevGraph &g, const DevState &st, const PhysTile &pt, int it,
+                                       int *active_count, int max_iter, hipStream_t s);
 // Monte-Carlo compaction of the running frames into tiles < nt (the finished ones counted first)
 hipError_t launch_phys_compact(const DevGraph &g, const DevState &st, const PhysTile &pt, int nt, int cap, int *pairs,
                                hipStream_t s);
