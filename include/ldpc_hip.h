@@ -205,7 +205,10 @@ int ldpc_phys_decode(const ldpc_graph *g, int32_t batch, const double *llr, int3
  * ldpc_mc_run (slot [5] unused).  The frame source is d_std's graph: either
  * the code's H_std = [A|I] (same generator as ldpc_mc_run), or -- for an IRA
  * code H = [H_info | staircase] such as the DVB-S2-profile code -- g_phys
- * itself (d_std created on g_phys; parities by accumulation). */
+ * itself (d_std created on g_phys; parities by accumulation).  On the HBM
+ * path the running frames of a chunk are compacted into its first tiles once
+ * at most a quarter of the slots still run (the finished frames counted
+ * first): the counters are those of the uncompacted decode. */
 int ldpc_phys_mc_run(ldpc_decoder *d_std, const ldpc_graph *g_phys, uint64_t seed, int32_t n_points,
                      const double *sigmas, int64_t frames_per_point, int64_t frame0, int32_t max_iter,
                      uint32_t flags, int64_t *counters_out, void *stream);
