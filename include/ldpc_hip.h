@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define LDPC_ABI_VERSION 4  /* 4: profile kinds of the few-frame / column-parallel kernels (LDPC_K_NKINDS 11) */
+#define LDPC_ABI_VERSION 5  /* 5: LDPC_F_TEST_ZERO + ldpc_rare_rows_read (4: profile kinds LDPC_K_NKINDS 11) */
 
 /* error codes */
 #define LDPC_OK 0
@@ -47,6 +47,11 @@ extern "C" {
 #define LDPC_F_PHYS_HBM 0x8u    /* physical mode: HBM-resident state even if LDS fits */
 #define LDPC_F_SPLIT 0x10u      /* parity decoder: separate CN/VN launches per iteration even
                                    where the tile-resident decoder applies (A/B, tests) */
+#define LDPC_F_TEST_ZERO 0x20u  /* TEST ONLY (ldpc_generate_frames, ldpc_mc_run): frames whose global
+                                   index F has F % 4 == 1 get a channel LLR of exactly 0.0 on identity
+                                   column k + (131 F + 7) mod m and information column (37 F + 3) mod k,
+                                   so their rows take spa_decoder.py:159-164's |t| <= 1e-10 branch (an
+                                   identity column's M = (0 + E) - E is 0 on every iteration) */
 
 typedef struct ldpc_hstd ldpc_hstd;       /* standard-form parity-check matrix  */
 typedef struct ldpc_graph ldpc_graph;     /* H_std uploaded to one GPU          */
@@ -235,6 +240,12 @@ int ldpc_phys_mc_run(ldpc_decoder *d_std, const ldpc_graph *g_phys, uint64_t see
 #define LDPC_K_NKINDS 11
 int ldpc_profile_enable(ldpc_decoder *d, int enable);
 int ldpc_profile_read(ldpc_decoder *d, double *ms_out, int64_t *launches_out);
+/* Rare rows (some |t| <= 1e-10, spa_decoder.py:159-164) this decoder has taken
+ * since the last call, then reset (synchronises the device): out[0] = rows
+ * queued to the split path's cn_rare_kernel (one per tile/row and iteration),
+ * out[1] = rare rows the tile-resident decoders took in-kernel (one per
+ * workgroup, row and pass).  A test hook: which code path saw the branch. */
+int ldpc_rare_rows_read(ldpc_decoder *d, int64_t *out);
 
 /* ------------------------------------------------ multi-GPU (RCCL, xGMI)
  * One process per GPU; frames are sharded by global index, so the only

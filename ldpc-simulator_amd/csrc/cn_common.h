@@ -77,6 +77,21 @@ __device__ __forceinline__ void fill_math_lds(MathLds &m) {
 // makes cn_row_kernel and tile_kernel spill; tile_sub.hip and tile8.hip use it.)
 __device__ __forceinline__ double cn_tanh(double M, const LdsTanh &t) { return clip_cl(np_tanh(M * 0.5, t)); }
 
+// atanh_f's 16 polynomial / log2 coefficients in constant memory, loaded with
+// two s_load_dwordx16 right where a kernel runs atanh_f.  The asm makes the
+// address opaque so the loads are not hoisted out of the row loop: passed as a
+// kernel argument (or hoisted) they would hold 32 SGPRs for the whole kernel,
+// which in the row-pipeline decoders spills other uniforms into VGPR lanes and
+// reloads them with v_readlane in the loop.
+static __constant__ AtanhCoef kAtanhCoefK = kAtanhCoef;
+typedef __attribute__((address_space(4))) const AtanhCoef ConstCoef;
+__device__ __forceinline__ AtanhCoef coef_load() {
+    ConstCoef *p = (ConstCoef *)&kAtanhCoefK;
+    asm volatile("" : "+s"(p));
+    return {p->t15, p->t13, p->t11, p->t9, p->t7, p->t5, p->t3, p->l8,
+            p->l7,  p->l6,  p->l5,  p->l4, p->l3, p->l2, p->ln2hi, p->ln2lo};
+}
+
 
 }  // namespace
 }  // namespace ldpc

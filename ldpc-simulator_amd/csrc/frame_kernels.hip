@@ -141,7 +141,7 @@ __global__ __launch_bounds__(64) void frame_channel_kernel(DevGraph g, DevState 
             const int w = r >> 5;
             const uint32_t bit = j < g.k ? (Ut[(j >> 5) * kTile] >> (j & 31)) & 1u
                                          : ((Pt[w * kTile] >> (r & 31)) ^ (Wt[(w >> 5) * kTile] >> (w & 31))) & 1u;
-            const double llr = valid ? channel_llr(bit, gz[q], s2) : 0.0;
+            const double llr = valid && !test_zero_llr(g, F, j) ? channel_llr(bit, gz[q], s2) : 0.0;
             if (to_lambda) {
                 Lamt[j * kTile] = -(float)llr;
                 Lt[j * kTile] = -(float)llr;
@@ -182,7 +182,7 @@ __global__ __launch_bounds__(64) void frame_channel_row_kernel(DevGraph g, DevSt
         const int w = r >> 5;
         const uint32_t bit = j < g.k ? (Ut[(j >> 5) * kTile] >> (j & 31)) & 1u
                                      : ((Pt[w * kTile] >> (r & 31)) ^ (Wt[(w >> 5) * kTile] >> (w & 31))) & 1u;
-        row_out[(size_t)f * g.n + j] = -(float)channel_llr(bit, gz[q], s2);
+        row_out[(size_t)f * g.n + j] = test_zero_llr(g, frame0 + f, j) ? -0.0f : -(float)channel_llr(bit, gz[q], s2);
     }
 }
 

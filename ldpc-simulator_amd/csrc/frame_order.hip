@@ -90,7 +90,7 @@ __global__ __launch_bounds__(kScoreThreads) void frame_score_kernel(DevGraph g, 
                     for (int w = 0; w < kw; ++w) acc ^= ar[w] & u[w];
                     bit = (uint32_t)__popc(acc) & 1u;
                 }
-                const double l = channel_llr(bit, gz[q], s2);
+                const double l = test_zero_llr(g, F, j) ? 0.0 : channel_llr(bit, gz[q], s2);
                 if (l > 0.0) hv |= 1u << q;
                 if (g.lpt_weak_id && j >= g.k && ((g.row_ptr[j - g.k + 1] - g.row_ptr[j - g.k]) & 1))
                     weak = fminf(weak, (float)fabs(l));
@@ -126,7 +126,8 @@ __global__ __launch_bounds__(kScoreThreads) void frame_score_kernel(DevGraph g, 
             }
             // |llr| >= 0: its float bits rise with it; the top 16 of 31, inverted
             const uint32_t rel = g.lpt_weak_id ? 0xffffu - (__float_as_uint(w) >> 15) : 0u;
-            score[f] = (s << 16) | rel;
+            // the weight saturates at 16 bits (launch_frame_order also rejects m > 65535)
+            score[f] = (min(s, 0xffffu) << 16) | rel;
             idx[f] = f;
         }
         __syncthreads();  // u / hb / wsum are rewritten by the next frame

@@ -53,6 +53,22 @@ __device__ __forceinline__ double channel_llr(uint32_t bit, double g, double s2)
     return (2.0 * y) / s2;
 }
 
+// Test-only erasures (LDPC_F_TEST_ZERO; tests/test_gpu_rare_stream.py): with
+// g.zinj != 0, frames F with F % 4 == 1 get a channel LLR of exactly 0.0 on
+// identity column k + (131 F + 7) mod m and on information column
+// (37 F + 3) mod k.  An identity column has degree 1 in H_std = [A | I], so
+// its M = L - E = (0 + E) - E is exactly 0 on EVERY iteration: the row takes
+// the reference's |t| <= 1e-10 branch (spa_decoder.py:159-164) on each pass
+// the frame makes -- in the streaming kernels and, for frames still running
+// at hand-off, in the split tail (cn_sub_kernel -> cn_rare_kernel).  The
+// information column does the same on the frame's first pass.  The predicate
+// is restated in the test, which checks the generator against it.
+__device__ __forceinline__ bool test_zero_llr(const DevGraph &g, long long F, int j) {
+    if (!g.zinj || (F & 3) != 1) return false;
+    const unsigned long long u = (unsigned long long)F;
+    return j == g.k + (int)((131ull * u + 7ull) % (unsigned long long)g.m) ||
+           (g.k > 0 && j == (int)((37ull * u + 3ull) % (unsigned long long)g.k));
+}
 
 __device__ __forceinline__ unsigned long long wave_sum(unsigned long long v) {
 #pragma unroll
@@ -118,7 +134,7 @@ __device__ inline void gen_slots(const DevGraph &g, const DevState &st, int tile
                     for (int w = 0; w < kw; ++w) acc ^= ar[w] & ustage[w * F + f];
                     bit = (uint32_t)__popc(acc) & 1u;
                 }
-                const double llr = channel_llr(bit, gz[q], s2);
+                const double llr = test_zero_llr(g, Fi, j) ? 0.0 : channel_llr(bit, gz[q], s2);
                 Ct[(size_t)j * kTile] = llr;
                 Lt[(size_t)j * kTile] = llr;
             }

@@ -54,7 +54,7 @@ struct ldpc_decoder {
     const ldpc_graph *g = nullptr;
     int cap_tiles = 0;
     double *E = nullptr, *T = nullptr, *L = nullptr, *ch = nullptr;
-    int *rare = nullptr;  // rare_count[2] + rare_list[cap_tiles*m]
+    int *rare = nullptr;  // rare_count[2] + running totals[2] (ldpc_rare_rows_read) + rare_list[cap_tiles*m*4]
     int nslots = 0;
     int *ints = nullptr;  // done, conv, status, iters, nllr_cnt, fresh, refill (cap frames each) + tile_active
     uint32_t *ubits = nullptr;
@@ -227,7 +227,7 @@ void state_bind(ldpc_decoder *d, int ntiles, int count) {
     s.T = d->T;
     s.rare_count = d->rare;
     s.active_count = nullptr;
-    s.rare_list = d->rare + 2;
+    s.rare_list = d->rare + 4;
     s.nslots = d->nslots;
     s.L = d->L;
     s.ch = d->ch;
@@ -245,6 +245,14 @@ void state_bind(ldpc_decoder *d, int ntiles, int count) {
     s.hist_stride = 0;
     s.ntiles = ntiles;
     s.count = count;
+}
+
+// The graph as one call sees it: LDPC_F_TEST_ZERO switches on the frame
+// source's test-only erasures (frame_source.h test_zero_llr) for this call only.
+DevGraph call_graph(const ldpc_decoder *d, uint32_t flags) {
+    DevGraph G = d->g->dg;
+    G.zinj = (flags & LDPC_F_TEST_ZERO) ? 1 : 0;
+    return G;
 }
 
 hipEvent_t take_event(ldpc_decoder *d) {
@@ -411,7 +419,7 @@ size_t workspace_bytes(const DevGraph &g, int cap_tiles) {
     b += cap * (size_t)g.nnz * 8;                                   // E
     const size_t slots = ldpc::use_tile(g) ? std::max(scratch_slots(), cap_tiles * tile_scratch_rows(g)) : scratch_slots();
     b += slots * g.max_row_deg * kTile * 8;  // T pool
-    b += 4 * (2 + (size_t)cap_tiles * g.m * 4);                           // rare list
+    b += 4 * (4 + (size_t)cap_tiles * g.m * 4);                           // rare counts + list
     b += 2 * cap * (size_t)g.n * 8;    // L, ch
     b += (7 * cap + cap_tiles) * 4;    // per-frame ints + tile flags
     b += cap * kw * 4;                 // ubits
@@ -570,7 +578,7 @@ int ldpc_graph_create(int32_t m, int32_t n, const int32_t *row_ptr, const int32_
     if (e != hipSuccess) {
         (void)hipFree(g->d_ints);
         (void)hipFree(g->d_apack);
-            delete g;
+        delete g;
         return ldpc_fail(LDPC_EDEVICE, "ldpc_graph_create: upload failed: %s", hipGetErrorString(e));
     }
     *out = g;
@@ -651,8 +659,8 @@ int ldpc_decoder_create(const ldpc_graph *g, int32_t max_frames, ldpc_decoder **
         return ldpc_fail(LDPC_ERANGE, "ldpc_decoder_create: %d frames x %d rows exceed the rare-row list", max_frames,
                          G.m);
     }
-    if (!rc) rc = dev_alloc(&d->rare, 2 + (size_t)d->cap_tiles * G.m * 4);
-    if (!rc && hipMemset(d->rare, 0, sizeof(int) * 2) != hipSuccess)
+    if (!rc) rc = dev_alloc(&d->rare, 4 + (size_t)d->cap_tiles * G.m * 4);
+    if (!rc && hipMemset(d->rare, 0, sizeof(int) * 4) != hipSuccess)
         rc = ldpc_fail(LDPC_EDEVICE, "ldpc_decoder_create: memset failed");
     if (!rc) rc = dev_alloc(&d->L, cap * (size_t)G.n);
     if (!rc) rc = dev_alloc(&d->ch, cap * (size_t)G.n);
@@ -848,7 +856,7 @@ int ldpc_decode_f64(ldpc_decoder *d, int32_t batch, const double *llr, int32_t m
 int ldpc_generate_frames(ldpc_decoder *d, uint64_t seed, int32_t snr_point, double sigma, int64_t frame0,
                          int32_t count, uint32_t flags, uint8_t *u_out, double *llr_out, void *stream) {
     if (!d) return ldpc_fail(LDPC_EINVAL, "ldpc_generate_frames: NULL decoder");
-    const DevGraph &G = d->g->dg;
+    const DevGraph G = call_graph(d, flags);
     if (!G.std_form && !G.ira)
         return ldpc_fail(LDPC_EINVAL, "ldpc_generate_frames: graph is neither [A | I_m] nor IRA [H_info | staircase]");
     if (count < 0 || count > d->cap_tiles * kTile || snr_point < 0 || frame0 < 0 || !(sigma > 0.0))
@@ -960,10 +968,9 @@ int ensure_order(ldpc_decoder *d, int64_t total) {
 // (refill_kernel), so no slot waits for the slowest frame of its tile or
 // chunk; only the last frames of the point form a tail.  Frames, and the
 // counters summed over them, are exactly the static schedule's.
-int mc_stream_point(ldpc_decoder *d, uint64_t seed, int p, double sigma, int64_t total, int64_t frame0, int max_iter,
-                    bool nllr, bool split, hipStream_t s) {
+int mc_stream_point(ldpc_decoder *d, const DevGraph &G, uint64_t seed, int p, double sigma, int64_t total,
+                    int64_t frame0, int max_iter, bool nllr, bool split, hipStream_t s) {
     if (total == 0) return LDPC_OK;
-    const DevGraph &G = d->g->dg;
     const int ntiles = (int)std::min<int64_t>(d->cap_tiles, (total + kTile - 1) / kTile);
     const int *order = nullptr;  // supply order (null: frame index order)
     // only when frames wait for a slot: with every frame running from the
@@ -1114,7 +1121,7 @@ int ldpc_mc_run(ldpc_decoder *d, uint64_t seed, int32_t n_points, const double *
                 int64_t frame0, int32_t max_iter, uint32_t flags, int64_t *counters_out, void *stream) {
     if (!d || n_points <= 0 || !sigmas || frames_per_point < 0 || frame0 < 0 || max_iter < 1 || !counters_out)
         return ldpc_fail(LDPC_EINVAL, "ldpc_mc_run: bad arguments");
-    const DevGraph &G = d->g->dg;
+    const DevGraph G = call_graph(d, flags);
     if (!G.std_form) return ldpc_fail(LDPC_EINVAL, "ldpc_mc_run: graph is not [A | I_m]");
     for (int p = 0; p < n_points; ++p)
         if (!(sigmas[p] > 0.0)) return ldpc_fail(LDPC_EINVAL, "ldpc_mc_run: sigma[%d] <= 0", p);
@@ -1134,7 +1141,7 @@ int ldpc_mc_run(ldpc_decoder *d, uint64_t seed, int32_t n_points, const double *
     const int64_t cap = (int64_t)d->cap_tiles * kTile;
     if (!(flags & LDPC_F_STATIC)) {
         for (int p = 0; p < n_points; ++p)
-            if (int rc = mc_stream_point(d, seed, p, sigmas[p], frames_per_point, frame0, max_iter, nllr,
+            if (int rc = mc_stream_point(d, G, seed, p, sigmas[p], frames_per_point, frame0, max_iter, nllr,
                                          flags & LDPC_F_SPLIT, s))
                 return rc;
     } else {
@@ -1159,6 +1166,18 @@ int ldpc_mc_run(ldpc_decoder *d, uint64_t seed, int32_t n_points, const double *
     HIP_TRY(hipMemcpyAsync(h.data(), d->counters, sizeof(unsigned long long) * need, hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
     for (int i = 0; i < need; ++i) counters_out[i] = (int64_t)h[i];
+    return LDPC_OK;
+}
+
+int ldpc_rare_rows_read(ldpc_decoder *d, int64_t *out) {
+    if (!d || !out) return ldpc_fail(LDPC_EINVAL, "ldpc_rare_rows_read: bad arguments");
+    DeviceGuard dg(d->g->device);
+    int h[2] = {0, 0};
+    HIP_TRY(hipDeviceSynchronize());
+    HIP_TRY(hipMemcpy(h, d->rare + 2, sizeof h, hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemset(d->rare + 2, 0, sizeof h));
+    out[0] = h[0];
+    out[1] = h[1];
     return LDPC_OK;
 }
 
@@ -1245,6 +1264,11 @@ int phys_tile_decode(ldpc_decoder *d, const DevGraph &P, int max_iter, bool from
     DevState st = d->st;  // st.ntiles shrinks with each compaction
     const PhysTile pt = phys_tile(d);
     const int cap = d->cap_tiles * kTile;
+    // LDPC_PHYS_COMPACT=0: no compaction (A/B, diagnosis; the counters are the same)
+    const bool compact = [] {
+        const char *e = getenv("LDPC_PHYS_COMPACT");
+        return !e || atoi(e) != 0;
+    }();
     HIP_TRY(hipMemsetAsync(d->pactive, 0, sizeof(int) * 2 * max_iter, s));
     HIP_TRY(ldpc::launch_phys_tile_init(P, st, pt, from_ch, s));
     for (int it = 0; it < max_iter; ++it) {
@@ -1270,7 +1294,7 @@ int phys_tile_decode(ldpc_decoder *d, const DevGraph &P, int max_iter, bool from
             if (running[0] == 0) break;  // every frame has stopped (converged; final() leaves them alone)
             const int nt = (running[1] + kTile - 1) / kTile;
             // (a quarter: half measured the same, profiles/r5_ab/r5am_ab)
-            if (ctr && nt < st.ntiles && 4 * (int64_t)running[1] <= (int64_t)st.ntiles * kTile) {
+            if (ctr && compact && nt < st.ntiles && 4 * (int64_t)running[1] <= (int64_t)st.ntiles * kTile) {
                 if (!d->cpairs && dev_alloc(&d->cpairs, 1 + 2 * (size_t)cap)) return LDPC_ENOMEM;
                 HIP_TRY(timed(d, LDPC_K_COUNT, s, [&] { return ldpc::launch_phys_tile_count(P, st, pt, ctr, s); }));
                 HIP_TRY(ldpc::launch_phys_compact(P, st, pt, nt, cap, d->cpairs, s));

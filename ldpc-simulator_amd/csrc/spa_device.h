@@ -46,6 +46,8 @@ struct DevGraph {
     int t8pair;                // tile8.hip runs its pair form (two rows per wavefront) on this graph
     int lpt_weak_id;           // frame_order.hip: rank equal syndromes by the weakest identity bit of an
                                // odd-degree row (set when at most half the rows have odd degree)
+    int zinj;                  // test-only erasure injection of the frame source (LDPC_F_TEST_ZERO): 0 = off,
+                               // else frame_source.h test_zero_llr (set per call, never on the graph itself)
 };
 
 // E layout inside a tile: the 64 frames in blocks of g.ef, each block
@@ -64,7 +66,8 @@ struct DevState {
     const int *order;        // streaming Monte-Carlo: local frame index of supply position i (frame_order.hip:
                              // heaviest syndrome first), or null: frame index order
     int *rare_list;          // [ntiles*m] tile*m+row of rows left to cn_rare_kernel
-    int *rare_count;         // [2] per iteration parity
+    int *rare_count;         // [2] per iteration parity, then two running totals (ldpc_rare_rows_read):
+                             // [2] rows cn_rare_kernel took, [3] rare rows the tile decoders took in-kernel
     int *active_count;       // [max_iter] or null: vn_kernel adds the tiles still running after it
     int nslots;
     uint32_t *ubits;         // MC only (may be null)
@@ -120,7 +123,8 @@ bool tile8_applies(const DevGraph &g);
 // whether tile8.hip's pair form can run this graph (set DevGraph::t8pair from it at graph creation)
 bool tile8_pair_fits(const DevGraph &g);
 size_t tile8_lds_bytes(const DevGraph &g);
-// rare-row scratch rows per tile it needs (1, or 2 for its pair form)
+// rare-row scratch rows per tile it needs: 2, or 4 for its pair form (two alternating
+// rare-row buffers per row slot)
 int tile8_scratch_per_tile(const DevGraph &g);
 hipError_t launch_tile8(const DevGraph &g, const DevState &st, int max_iter, bool nllr, hipStream_t s);
 // its streaming Monte-Carlo form (one persistent launch per SNR point, handoff as launch_tile_stream)

@@ -306,6 +306,7 @@ __global__ __launch_bounds__(256) void cn_rare_kernel(DevGraph g, DevState st, i
     const int count = st.rare_count[it_parity];
     if (blockIdx.x == 0 && threadIdx.x == 0) st.rare_count[it_parity ^ 1] = 0;  // for the next CN
     if (count == 0) return;  // block-uniform
+    if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(&st.rare_count[2], count);  // ldpc_rare_rows_read
     fill_math_lds(mlds);
     __syncthreads();
     const LdsTanh ttab{mlds.tanh};

@@ -1192,6 +1192,7 @@ __global__ __launch_bounds__(64 * kW8, 1) void tile8_kernel(DevGraph g, DevState
         __syncthreads();
         if (!flags[2 * NS + 1]) break;
     }
+    count_rare_rows(st, c.tseq, kW8);
 #ifdef LDPC_T8_TIMERS
     if ((blockIdx.x == 0 || blockIdx.x == 777) && (threadIdx.x & 63) == 0)
         printf("T8 b=%d w=%d hopw=%llu hop=%llu p3f=%llu p3m=%llu p3o=%llu p3s=%llu p1=%llu pre=%llu rows=%llu\n",
@@ -1370,6 +1371,7 @@ __global__ __launch_bounds__(64 * kW8, 1) void tile8_stream_kernel(
         __syncthreads();  // wave 0 has read zb (error bits) before it is cleared
         for (int i = threadIdx.x; i < (kw + mw) * kF8; i += blockDim.x) zb[i] = 0u;
     }
+    count_rare_rows(st, c.tseq, kW8);
 }
 
 // Variants: (K, L_A in LDS, pipeline depth D, pair form).  wimax_2304_0.5:

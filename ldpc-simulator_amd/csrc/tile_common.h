@@ -8,11 +8,23 @@
 #include <cstddef>
 
 #include "cn_common.h"
+#include "spa_device.h"
 
 namespace ldpc {
 namespace {
 
 __host__ __device__ inline size_t al16(size_t x) { return (x + 15) & ~(size_t)15; }
+
+// End of a tile decoder (every wavefront arrives): the rare rows it took in
+// kernel -- its LDS rare-row sequence counts one per wavefront and rare row --
+// into the decoder's running total (DevState::rare_count[3], ldpc_rare_rows_read).
+__device__ __forceinline__ void count_rare_rows(const DevState &st, const int *tseq, int waves) {
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const int n = *tseq / waves;
+        if (n) atomicAdd(&st.rare_count[3], n);
+    }
+}
 
 __device__ __forceinline__ int lds_ld(const int *p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);

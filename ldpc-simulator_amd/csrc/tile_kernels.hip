@@ -461,6 +461,7 @@ __global__ __launch_bounds__(64 * kTW, 1) void tile_kernel(DevGraph g, DevState 
                            kTW, c.live))
             break;
     }
+    count_rare_rows(st, c.tseq, kTW);
 }
 
 
@@ -673,6 +674,7 @@ __global__ __launch_bounds__(64 * kTW, 1) void tile_stream_kernel(DevGraph g, De
         for (int i = threadIdx.x; i < mw * kTile; i += blockDim.x) ib[i] = 0u;
         // zb is reused as the u-bit stage and cleared at the top of the loop
     }
+    count_rare_rows(st, c.tseq, kTW);
 }
 
 }  // namespace

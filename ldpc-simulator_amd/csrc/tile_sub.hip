@@ -66,6 +66,11 @@ constexpr int kSW = kSubWaves;
 #define SUB_ADD(c, i, a, b)
 #endif
 constexpr size_t kSubLdsMax = 163840;
+#ifdef LDPC_SUB_COEF
+#define SUB_COEF(c) coef_load()
+#else
+#define SUB_COEF(c) (c).ac
+#endif
 
 template <int Q>
 struct SubCfg {
@@ -498,9 +503,10 @@ __device__ __forceinline__ void sub_p3_body(SubCtx<Q> &c, int r, double (&t)[Sub
             for (int i = 0; i < K; ++i)
                 if (i < rc.CS) t[i] = 2.0 * t[i];
         } else {
+            const AtanhCoef ac = SUB_COEF(c);
 #pragma unroll
             for (int i = 0; i < K; ++i)
-                if (i < rc.CS) t[i] = 2.0 * atanh_f(clip_cl(t[i]), c.ltab, c.ac);
+                if (i < rc.CS) t[i] = 2.0 * atanh_f(clip_cl(t[i]), c.ltab, ac);
         }
     } else {
         // rare: q = in-order product of the others (np.prod(np.delete(...)),
@@ -514,6 +520,7 @@ __device__ __forceinline__ void sub_p3_body(SubCtx<Q> &c, int r, double (&t)[Sub
         c.ntiny += 1;
         if ((threadIdx.x & 63) == 0) __hip_atomic_fetch_add(c.tseq, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
         wait_flag<false>(c.tseq, c.ntiny * kSW);
+        const AtanhCoef ac = SUB_COEF(c);
 #pragma unroll
         for (int i = 0; i < K; ++i) {
             if (i < rc.CS) {
@@ -532,7 +539,7 @@ __device__ __forceinline__ void sub_p3_body(SubCtx<Q> &c, int r, double (&t)[Sub
                         fst = false;
                     }
                 }
-                t[i] = 2.0 * atanh_f(clip_cl(q), c.ltab, c.ac);
+                t[i] = 2.0 * atanh_f(clip_cl(q), c.ltab, ac);
             }
         }
     }
@@ -783,6 +790,7 @@ __global__ __launch_bounds__(64 * kSW, 1) void tile_sub_kernel(DevGraph g, DevSt
         __syncthreads();
         if (!flags[2 * kSR + 1]) break;
     }
+    count_rare_rows(st, c.tseq, kSW);
 #ifdef LDPC_SUB_TIMERS
     if ((blockIdx.x == 0 || blockIdx.x == 777) && (threadIdx.x & 63) == 0)
         printf("SUB b=%d w=%d hopw=%llu hop=%llu p3f=%llu p3m=%llu p3o=%llu p3s=%llu p1=%llu\n", (int)blockIdx.x,
@@ -1016,6 +1024,7 @@ __global__ __launch_bounds__(64 * kSW, 1) void tile_sub_stream_kernel(
         for (int i = threadIdx.x; i < (kw + mw) * F; i += blockDim.x) zb[i] = 0u;
         __syncthreads();
     }
+    count_rare_rows(st, c.tseq, kSW);
 }
 
 template <int Q>

@@ -27,6 +27,7 @@ LDPC_F_DEVICE_PTRS = 0x2
 LDPC_F_STATIC = 0x4
 LDPC_F_PHYS_HBM = 0x8
 LDPC_F_SPLIT = 0x10
+LDPC_F_TEST_ZERO = 0x20  # test only: frame-source erasures (include/ldpc_hip.h)
 LDPC_MC_NCOUNT = 7
 LDPC_EINVAL = -22  # include/ldpc_hip.h error codes used on the Python side
 LDPC_ERANGE = -34
@@ -39,7 +40,7 @@ EXPORTED = (
     "ldpc_phys_kernel_name", "ldpc_tile_lds_bytes", "ldpc_tile_kernel_name",
     "ldpc_decoder_bytes", "ldpc_decoder_create", "ldpc_decoder_destroy", "ldpc_decoder_capacity",
     "ldpc_decode_f64", "ldpc_generate_frames", "ldpc_mc_run", "ldpc_frame_order",
-    "ldpc_profile_enable", "ldpc_profile_read",
+    "ldpc_profile_enable", "ldpc_profile_read", "ldpc_rare_rows_read",
     "ldpc_phys_lds_bytes", "ldpc_phys_decode", "ldpc_phys_mc_run",
     "ldpc_comm_unique_id", "ldpc_comm_init", "ldpc_comm_allreduce", "ldpc_comm_barrier", "ldpc_comm_destroy",
     "ldpc_device_synchronize",
@@ -97,6 +98,7 @@ def _declare(lib):
         "ldpc_phys_mc_run": (ctypes.c_int, [c_vp, c_vp, c_u64, c_i32, P(c_dbl), c_i64, c_i64, c_i32, c_u32,
                                             P(c_i64), c_vp]),
         "ldpc_profile_read": (ctypes.c_int, [c_vp, P(c_dbl), P(c_i64)]),
+        "ldpc_rare_rows_read": (ctypes.c_int, [c_vp, P(c_i64)]),
         "ldpc_comm_unique_id": (ctypes.c_int, [c_vp]),
         "ldpc_comm_init": (ctypes.c_int, [c_vp, c_i32, c_i32, c_i32, P(c_vp)]),
         "ldpc_comm_allreduce": (ctypes.c_int, [c_vp, c_vp, c_i64, c_i32, c_i32, c_u32, c_vp]),

@@ -208,25 +208,29 @@ class Decoder:
             self._h, B, dp(llr), int(max_iter), flags, dp(z), dp(conv), dp(status), dp(post), dp(nllr), dp(hist),
             dp(iters), None, ctypes.c_void_p(int(stream)) if stream else None))
 
-    def generate(self, seed, snr_point, sigma, frame0, count):
-        """On-device synthetic frames (u bits, channel LLRs) copied back for testing."""
+    def generate(self, seed, snr_point, sigma, frame0, count, test_zero=False):
+        """On-device synthetic frames (u bits, channel LLRs) copied back for testing.
+        test_zero: the frame source's test-only erasures (LDPC_F_TEST_ZERO)."""
         g = self.graph
         u = np.empty((count, g.k), np.uint8)
         llr = np.empty((count, g.n), np.float64)
         check("ldpc_generate_frames", _lib.gpu().ldpc_generate_frames(
-            self._h, int(seed), int(snr_point), float(sigma), int(frame0), int(count), 0,
-            _lib.ptr(u), _lib.ptr(llr), None))
+            self._h, int(seed), int(snr_point), float(sigma), int(frame0), int(count),
+            _lib.LDPC_F_TEST_ZERO if test_zero else 0, _lib.ptr(u), _lib.ptr(llr), None))
         return u, llr
 
-    def mc_run(self, seed, sigmas, frames_per_point, frame0, max_iter, nllr=False, static=False, split=False):
+    def mc_run(self, seed, sigmas, frames_per_point, frame0, max_iter, nllr=False, static=False, split=False,
+               test_zero=False):
         """Generate + decode + count on the GPU; returns int64 [n_points, 7] counters.
 
         Default schedule streams frames through the decoder's slots (a slot is
         refilled as soon as its frame stops); static=True decodes chunks of
-        capacity frames to completion.  Same frames, identical counters."""
+        capacity frames to completion.  Same frames, identical counters.
+        test_zero: the frame source's test-only erasures (LDPC_F_TEST_ZERO)."""
         sig = np.ascontiguousarray(np.asarray(sigmas, dtype=np.float64))
         out = np.zeros((len(sig), LDPC_MC_NCOUNT), np.int64)
-        flags = (LDPC_F_NLLR if nllr else 0) | (LDPC_F_STATIC if static else 0) | (LDPC_F_SPLIT if split else 0)
+        flags = (LDPC_F_NLLR if nllr else 0) | (LDPC_F_STATIC if static else 0) | (LDPC_F_SPLIT if split else 0) | \
+            (_lib.LDPC_F_TEST_ZERO if test_zero else 0)
         check("ldpc_mc_run", _lib.gpu().ldpc_mc_run(
             self._h, int(seed), len(sig), sig.ctypes.data_as(ctypes.POINTER(ctypes.c_double)),
             int(frames_per_point), int(frame0), int(max_iter), flags,
@@ -267,6 +271,13 @@ class Decoder:
         n = (ctypes.c_int64 * len(self.KINDS))()
         check("ldpc_profile_read", _lib.gpu().ldpc_profile_read(self._h, ms, n))
         return {k: (ms[i], n[i]) for i, k in enumerate(self.KINDS)}
+
+    def rare_rows(self):
+        """(rows queued to cn_rare_kernel, rare rows the tile decoders took in-kernel)
+        since the last call (ldpc_rare_rows_read)."""
+        out = (ctypes.c_int64 * 2)()
+        check("ldpc_rare_rows_read", _lib.gpu().ldpc_rare_rows_read(self._h, out))
+        return int(out[0]), int(out[1])
 
     def close(self):
         h = getattr(self, "_h", None)

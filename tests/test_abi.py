@@ -45,7 +45,7 @@ def test_library_has_gfx950_code_object():
 
 
 def test_abi_version():
-    assert _lib.lib().ldpc_abi_version() == 4
+    assert _lib.lib().ldpc_abi_version() == 5
 
 
 def test_no_gpu_means_loud_failure():

@@ -65,8 +65,11 @@ def _graph(H):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("name,snr,B", [("wimax_576_0.5", -2.5, 192), ("wimax_2304_0.5", -2.5, 96),
-                                         ("wimax_2304_0.75A", -1.0, 96)])
+                                         ("wimax_2304_0.75A", -1.0, 96), ("wimax_576_0.5", 0.0, 192)])
 def test_hbm_path_bit_identical_to_lds(gpu_available, name, snr, B):
+    """The 0 dB case pins the HBM path's early syndrome (phys_tile_syn_kernel /
+    phys_tile_exit_kernel after VN(1) and VN(2): conv = it, iters = it + 1) to
+    the LDS kernel frame by frame."""
     from ldpc_amd.device import phys_decode
     edd = ldpc_amd.load_committed_code(name)
     Hp = edd.physical_matrix()
@@ -74,15 +77,17 @@ def test_hbm_path_bit_identical_to_lds(gpu_available, name, snr, B):
     g = _graph(Hp)
     a = phys_decode(g, llr, 50, post=True)
     b = phys_decode(g, llr, 50, post=True, hbm=True)
-    if name == "wimax_576_0.5":
+    if name == "wimax_576_0.5" and snr < 0:
         assert 0 < (a.status == 0).sum() < B  # a mix of outcomes (waterfall)
+    if snr >= 0:  # frames that stop at the early syndrome after VN(1) / VN(2)
+        assert np.isin(b.iters, (2, 3)).sum() > 0, np.bincount(b.iters)
     for key in ("z", "conv", "status", "iters"):
         np.testing.assert_array_equal(a[key], b[key], err_msg=key)
     np.testing.assert_array_equal(a.post.view(np.uint32), b.post.view(np.uint32))
 
 
 @pytest.mark.gpu
-def test_phys_mc_hbm_counters_equal_lds(gpu_available):
+def test_phys_mc_hbm_counters_equal_lds(gpu_available, monkeypatch):
     from ldpc_amd.device import Decoder
     edd = ldpc_amd.load_committed_code("wimax_576_0.5")
     dec = Decoder(_graph(edd._h_std), 1024)
@@ -98,6 +103,8 @@ def test_phys_mc_hbm_counters_equal_lds(gpu_available):
     # are counted before the move, so more count launches than chunks)
     chunks = 3 * 2
     assert p["count"][1] > chunks, p["count"]
+    monkeypatch.setenv("LDPC_PHYS_COMPACT", "0")  # the switch (A/B, diagnosis): same counters
+    np.testing.assert_array_equal(dec.phys_mc_run(gp, SEED, sig, 2000, 64, 50, hbm=True), a)
 
 
 @pytest.mark.gpu
