@@ -173,7 +173,6 @@ struct T8Ctx {
     int *flag, *tinyf, *tseq, *p3row;
     LdsTanh ttab;
     LdsAtanh ltab;
-    AtanhCoef ac;
     int m, k, wave, j, f, nnz;
     int h;  // pair form: this lane's row of the pair (lane = h*32 + j*8 + f); 0 otherwise
     int ep0;
@@ -413,6 +412,7 @@ __device__ __forceinline__ void t8_p3(T8Ctx<K> &c, int r, double (&t)[K]) {
     T8_STAMP(q1);
     T8_ADD(c, 2, q0, q1);
     const bool tiny_row = uniform(lds_ld(c.tinyf + s)) != 0;
+    const AtanhCoef ac = coef_load();  // scalar loads for this P3 only, not 32 SGPRs held (cn_common.h)
     const int nj = t8_nj(c, rc);
     const double tI = c.slot[(kSR8 + s) * kF8];
     const double P = c.slot[s * kF8] * tI;  // (t_0 * ... * t_{deg-2}) * t_id: left to right (:151-152)
@@ -423,7 +423,7 @@ __device__ __forceinline__ void t8_p3(T8Ctx<K> &c, int r, double (&t)[K]) {
         // kAtanhIdent), decided slot by slot
         const double lim = c.live ? kAtanhIdent : INFINITY;  // frame-less lanes do not vote
         auto en = [&](double q) {
-            return __ballot(!(fabs(q) < lim)) == 0ull ? 2.0 * q : 2.0 * atanh_f(clip_cl(q), c.ltab, c.ac);
+            return __ballot(!(fabs(q) < lim)) == 0ull ? 2.0 * q : 2.0 * atanh_f(clip_cl(q), c.ltab, ac);
         };
         if (div_nr_ok(c.live ? P : 1.0)) {  // the IEEE quotient without its scaling steps (cn_common.h)
             if (rc.cnt > 0) {
@@ -449,7 +449,7 @@ __device__ __forceinline__ void t8_p3(T8Ctx<K> &c, int r, double (&t)[K]) {
                             else if (i > 0 && __ballot(c.live && i < nj && fabs(q) != key) == 0ull)
                                 t[i] = dfrom((dbits(t[0]) & 0x7fffffffffffffffull) | (dbits(q) & 0x8000000000000000ull));
                             else
-                                t[i] = 2.0 * atanh_f(clip_cl(q), c.ltab, c.ac);
+                                t[i] = 2.0 * atanh_f(clip_cl(q), c.ltab, ac);
                         }
                                 }
                 } else {
@@ -501,13 +501,13 @@ __device__ __forceinline__ void t8_p3(T8Ctx<K> &c, int r, double (&t)[K]) {
                 if (i < rc.CS) {
                     const double ti = t[i];
                     const double q = (fabs(ti) > kTiny || i >= nj) ? P / ti : others(pos0 + i);
-                    t[i] = 2.0 * atanh_f(clip_cl(q), c.ltab, c.ac);
+                    t[i] = 2.0 * atanh_f(clip_cl(q), c.ltab, ac);
                 }
             }
         }
         if (idw) {
             const double q = fabs(tI) > kTiny ? P / tI : others(rc.deg - 1);
-            EI = 2.0 * atanh_f(clip_cl(q), c.ltab, c.ac);
+            EI = 2.0 * atanh_f(clip_cl(q), c.ltab, ac);
         }
     }
     {  // slots past the piece (and frames that stopped) store out of range: dropped (no branch)
@@ -812,6 +812,7 @@ __device__ __forceinline__ void tp_p3(T8Ctx<K> &c, int q, double (&t)[K], TpStag
     T8_STAMP(q1);
     T8_ADD(c, 2, q0, q1);
     const bool tiny_row = lds_ld(c.tinyf + s * 2 + c.h) != 0;
+    const AtanhCoef ac = coef_load();  // scalar loads for this P3 only (cn_common.h)
     const bool tiny_any = __ballot(tiny_row) != 0ull;
     const int nj = tp_nj(c, rc);
     const double tI = c.slot[(c.ns + s * 2 + c.h) * kF8];
@@ -889,8 +890,8 @@ __device__ __forceinline__ void tp_p3(T8Ctx<K> &c, int q, double (&t)[K], TpStag
             EI = 2.0 * EI;
         } else {
 #pragma unroll
-            for (int i = 0; i < K; ++i) t[i] = 2.0 * atanh_f(clip_cl(t[i]), c.ltab, c.ac);
-            EI = 2.0 * atanh_f(clip_cl(EI), c.ltab, c.ac);
+            for (int i = 0; i < K; ++i) t[i] = 2.0 * atanh_f(clip_cl(t[i]), c.ltab, ac);
+            EI = 2.0 * atanh_f(clip_cl(EI), c.ltab, ac);
         }
         finish(t, EI);
     } else {
@@ -935,12 +936,12 @@ __device__ __forceinline__ void tp_p3(T8Ctx<K> &c, int q, double (&t)[K], TpStag
             if (c.live) {
                 const double ti = t8_ld(c.rE, t8_es(c, eoff, i));
                 const double qv = (tiny_row && !(fabs(ti) > kTiny)) ? others(pos0 + i) : P / ti;
-                t8_st<kEStAux>(c.rE, t8_es(c, eoff, i), 2.0 * atanh_f(clip_cl(qv), c.ltab, c.ac));
+                t8_st<kEStAux>(c.rE, t8_es(c, eoff, i), 2.0 * atanh_f(clip_cl(qv), c.ltab, ac));
             }
         }
         if (idw) {
             const double qv = (!tiny_row || fabs(tI) > kTiny) ? P / tI : others(rc.deg - 1);
-            EI = 2.0 * atanh_f(clip_cl(qv), c.ltab, c.ac);
+            EI = 2.0 * atanh_f(clip_cl(qv), c.ltab, ac);
         }
         __builtin_amdgcn_s_waitcnt(0);
 #pragma unroll
@@ -983,7 +984,7 @@ __device__ __forceinline__ void tp_rows(T8Ctx<K> &c) {
 template <int K, bool LA, bool PAIR, int NS>
 __device__ __forceinline__ void t8_setup(T8Ctx<K> &c, unsigned char *lds, const T8Layout &ly, const DevGraph &g,
                                          const DevState &st, int tile, int sub, const int *col_idx,
-                                         const int *row_ptr, const AtanhCoef &ac) {
+                                         const int *row_ptr) {
     MathLds &mlds = *(MathLds *)(lds + ly.math);
     int *flags = (int *)(lds + ly.flags);
     const int lane = threadIdx.x & 63;
@@ -1018,7 +1019,6 @@ __device__ __forceinline__ void t8_setup(T8Ctx<K> &c, unsigned char *lds, const 
     c.p3row = flags + 2 * NS + 2;
     c.ttab = LdsTanh{mlds.tanh};
     c.ltab = LdsAtanh{mlds.atanh};
-    c.ac = ac;
     c.m = g.m;
     c.k = g.k;
     c.nnz = g.nnz;
@@ -1089,7 +1089,7 @@ __device__ __forceinline__ void t8_syndrome(const DevGraph &g, const uint32_t *z
 template <int K, bool LA, int D, bool PAIR = false>
 __global__ __launch_bounds__(64 * kW8, 1) void tile8_kernel(DevGraph g, DevState st, int max_iter, int nllr,
                                                             const int *__restrict__ col_idx,
-                                                            const int *__restrict__ row_ptr, AtanhCoef ac) {
+                                                            const int *__restrict__ row_ptr) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     constexpr int NS = t8_ns(PAIR, D);
     const T8Layout ly = t8_layout(g.k, g.m, K, LA, t8_ring(PAIR, D), NS);
@@ -1129,7 +1129,7 @@ __global__ __launch_bounds__(64 * kW8, 1) void tile8_kernel(DevGraph g, DevState
     }
 
     T8Ctx<K> c;
-    t8_setup<K, LA, PAIR, NS>(c, lds, ly, g, st, tile, sub, col_idx, row_ptr, ac);
+    t8_setup<K, LA, PAIR, NS>(c, lds, ly, g, st, tile, sub, col_idx, row_ptr);
     c.R = t8_ring(PAIR, D);
     // the identity edge's wavefront: with D = 3 wavefront 0, which otherwise
     // waits longest for the chain; with D = 2 the last one (wavefront 0's
@@ -1220,7 +1220,7 @@ __global__ __launch_bounds__(64 * kW8, 1) void tile8_kernel(DevGraph g, DevState
 template <int K, bool LA, int D, bool PAIR = false>
 __global__ __launch_bounds__(64 * kW8, 1) void tile8_stream_kernel(
     DevGraph g, DevState st, int max_iter, int nllr, const int *__restrict__ col_idx,
-    const int *__restrict__ row_ptr, AtanhCoef ac, uint64_t seed, int snr_point, double sigma, int64_t frame0,
+    const int *__restrict__ row_ptr, uint64_t seed, int snr_point, double sigma, int64_t frame0,
     int64_t total, unsigned long long *next, unsigned long long *ctr, int64_t handoff) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     __shared__ long long gidx[kF8];  // refill: slot f's new frame index (< 0: none)
@@ -1255,7 +1255,7 @@ __global__ __launch_bounds__(64 * kW8, 1) void tile8_stream_kernel(
     const __amdgpu_buffer_rsrc_t rL = t8_rsrc(st.L + (size_t)tile * g.n * kTile, (size_t)g.n * kTile * sizeof(double));
 
     T8Ctx<K> c;
-    t8_setup<K, LA, PAIR, NS>(c, lds, ly, g, st, tile, sub, col_idx, row_ptr, ac);
+    t8_setup<K, LA, PAIR, NS>(c, lds, ly, g, st, tile, sub, col_idx, row_ptr);
     c.R = t8_ring(PAIR, D);
     c.idwave = 0;  // as tile8_kernel
     const int m = g.m;
@@ -1444,17 +1444,17 @@ hipError_t launch_tile8_stream(const DevGraph &g, const DevState &st, int max_it
     switch (t8_variant(g)) {
         case 121:
             tile8_stream_kernel<10, true, 2, true><<<grid, block, lds, s>>>(g, st, max_iter, nllr ? 1 : 0, g.col_idx,
-                                                                         g.row_ptr, kAtanhCoef, seed, snr_point,
+                                                                         g.row_ptr, seed, snr_point,
                                                                          sigma, frame0, total, next, ctr, handoff);
             break;
         case 11:
             tile8_stream_kernel<5, true, kD5><<<grid, block, lds, s>>>(g, st, max_iter, nllr ? 1 : 0, g.col_idx,
-                                                                      g.row_ptr, kAtanhCoef, seed, snr_point, sigma,
+                                                                      g.row_ptr, seed, snr_point, sigma,
                                                                       frame0, total, next, ctr, handoff);
             break;
         case 16:
             tile8_stream_kernel<8, false, kD8><<<grid, block, lds, s>>>(g, st, max_iter, nllr ? 1 : 0, g.col_idx,
-                                                                       g.row_ptr, kAtanhCoef, seed, snr_point, sigma,
+                                                                       g.row_ptr, seed, snr_point, sigma,
                                                                        frame0, total, next, ctr, handoff);
             break;
         default:
@@ -1470,15 +1470,14 @@ hipError_t launch_tile8(const DevGraph &g, const DevState &st, int max_iter, boo
     switch (t8_variant(g)) {
         case 121:
             tile8_kernel<10, true, 2, true><<<grid, block, lds, s>>>(g, st, max_iter, nllr ? 1 : 0, g.col_idx,
-                                                                  g.row_ptr, kAtanhCoef);
+                                                                  g.row_ptr);
             break;
         case 11:
-            tile8_kernel<5, true, kD5><<<grid, block, lds, s>>>(g, st, max_iter, nllr ? 1 : 0, g.col_idx, g.row_ptr,
-                                                               kAtanhCoef);
+            tile8_kernel<5, true, kD5><<<grid, block, lds, s>>>(g, st, max_iter, nllr ? 1 : 0, g.col_idx, g.row_ptr);
             break;
         case 16:
             tile8_kernel<8, false, kD8><<<grid, block, lds, s>>>(g, st, max_iter, nllr ? 1 : 0, g.col_idx,
-                                                                g.row_ptr, kAtanhCoef);
+                                                                g.row_ptr);
             break;
         default:
             return hipErrorInvalidValue;

@@ -133,7 +133,6 @@ struct TileCtx {
     int *flag, *tinyf, *tseq;
     LdsTanh ttab;
     LdsAtanh ltab;
-    AtanhCoef ac;
     int k, wave;
     uint32_t lane;
     int ep0;  // epoch of row 0 in this pass (flags are tagged (epoch, stage))
@@ -233,10 +232,11 @@ __device__ __forceinline__ void tile_p3(TileCtx &c, int r, double (&t)[kTK]) {
     wait_flag(c.flag + s, ep + kTW);
     const double P = c.slot[s * kTile + c.lane];
     const bool tiny_row = uniform(lds_ld(c.tinyf + s)) != 0;
+    const AtanhCoef ac = coef_load();  // scalar loads for this P3 only (cn_common.h)
     if (!tiny_row) {
 #pragma unroll
         for (int i = 0; i < kTK; ++i)
-            if (i < rc.cnt) t[i] = 2.0 * atanh_f(clip_cl(P / t[i]), c.ltab, c.ac);  // :159-168
+            if (i < rc.cnt) t[i] = 2.0 * atanh_f(clip_cl(P / t[i]), c.ltab, ac);  // :159-168
     } else {
         // rare: q = prod of the others, in order (np.prod(np.delete(...)), :164)
         // the rare rows alternate between two scratch buffers: a wavefront
@@ -268,7 +268,7 @@ __device__ __forceinline__ void tile_p3(TileCtx &c, int r, double (&t)[kTK]) {
                         fst = false;
                     }
                 }
-                t[i] = 2.0 * atanh_f(clip_cl(q), c.ltab, c.ac);
+                t[i] = 2.0 * atanh_f(clip_cl(q), c.ltab, ac);
             }
         }
     }
@@ -374,7 +374,7 @@ __device__ __forceinline__ bool tile_pass_end(const DevGraph &g, const DevState 
 
 __global__ __launch_bounds__(64 * kTW, 1) void tile_kernel(DevGraph g, DevState st, int max_iter, int nllr,
                                                            const int *__restrict__ col_idx,
-                                                           const int *__restrict__ row_ptr, AtanhCoef ac) {
+                                                           const int *__restrict__ row_ptr) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     const TileLayout ly = tile_layout(g.k, g.m);
     double *S = (double *)(lds + ly.S);
@@ -418,7 +418,6 @@ __global__ __launch_bounds__(64 * kTW, 1) void tile_kernel(DevGraph g, DevState 
     c.tseq = flags + 2 * kTR;
     c.ttab = LdsTanh{mlds.tanh};
     c.ltab = LdsAtanh{mlds.atanh};
-    c.ac = ac;
     c.k = g.k;
     c.lane = lane;
     c.wave = wave;
@@ -503,7 +502,7 @@ __device__ __forceinline__ bool tile_refill(const DevState &st, int lane, bool w
 
 __global__ __launch_bounds__(64 * kTW, 1) void tile_stream_kernel(DevGraph g, DevState st, int max_iter, int nllr,
                                                                   const int *__restrict__ col_idx,
-                                                                  const int *__restrict__ row_ptr, AtanhCoef ac,
+                                                                  const int *__restrict__ row_ptr,
                                                                   uint64_t seed, int snr_point, double sigma,
                                                                   int64_t frame0, int64_t total,
                                                                   unsigned long long *next,
@@ -556,7 +555,6 @@ __global__ __launch_bounds__(64 * kTW, 1) void tile_stream_kernel(DevGraph g, De
     c.tseq = flags + 2 * kTR;
     c.ttab = LdsTanh{mlds.tanh};
     c.ltab = LdsAtanh{mlds.atanh};
-    c.ac = ac;
     c.k = g.k;
     c.lane = lane;
     c.wave = wave;
@@ -744,7 +742,7 @@ hipError_t launch_tile_stream(const DevGraph &g, const DevState &st, int max_ite
                                       handoff, s);
     if (!lds || !g.a_packed || !st.ubits || 2 * st.ntiles > st.nslots) return hipErrorInvalidValue;
     tile_stream_kernel<<<st.ntiles, 64 * kTW, lds, s>>>(g, st, max_iter, nllr ? 1 : 0, g.col_idx, g.row_ptr,
-                                                        kAtanhCoef, seed, snr_point, sigma, frame0, total, next, ctr);
+                                                        seed, snr_point, sigma, frame0, total, next, ctr);
     return hipGetLastError();
 }
 
@@ -753,7 +751,7 @@ hipError_t launch_tile(const DevGraph &g, const DevState &st, int max_iter, bool
     const size_t lds = tile64_lds_bytes(g);
     if (!lds && g.ef == 8) return launch_tile8(g, st, max_iter, nllr, s);
     if (!lds) return sub_enabled(g) ? launch_tile_sub(g, st, max_iter, nllr, s) : hipErrorInvalidValue;
-    tile_kernel<<<st.ntiles, 64 * kTW, lds, s>>>(g, st, max_iter, nllr ? 1 : 0, g.col_idx, g.row_ptr, kAtanhCoef);
+    tile_kernel<<<st.ntiles, 64 * kTW, lds, s>>>(g, st, max_iter, nllr ? 1 : 0, g.col_idx, g.row_ptr);
     return hipGetLastError();
 }
 

@@ -66,11 +66,7 @@ constexpr int kSW = kSubWaves;
 #define SUB_ADD(c, i, a, b)
 #endif
 constexpr size_t kSubLdsMax = 163840;
-#ifdef LDPC_SUB_COEF
-#define SUB_COEF(c) coef_load()
-#else
-#define SUB_COEF(c) (c).ac
-#endif
+
 
 template <int Q>
 struct SubCfg {
@@ -199,7 +195,6 @@ struct SubCtx {
     const int *p3dep;
     LdsTanh ttab;
     LdsAtanh ltab;
-    AtanhCoef ac;
     // uniform (SGPR) tile bases + this lane's byte offset: every access is a
     // 32-bit per-lane offset from a scalar base (global_load ... v_off, s_base)
     const char *Eu, *Lu, *Cu;
@@ -503,7 +498,7 @@ __device__ __forceinline__ void sub_p3_body(SubCtx<Q> &c, int r, double (&t)[Sub
             for (int i = 0; i < K; ++i)
                 if (i < rc.CS) t[i] = 2.0 * t[i];
         } else {
-            const AtanhCoef ac = SUB_COEF(c);
+            const AtanhCoef ac = coef_load();  // scalar loads here, not 32 SGPRs held (cn_common.h)
 #pragma unroll
             for (int i = 0; i < K; ++i)
                 if (i < rc.CS) t[i] = 2.0 * atanh_f(clip_cl(t[i]), c.ltab, ac);
@@ -520,7 +515,7 @@ __device__ __forceinline__ void sub_p3_body(SubCtx<Q> &c, int r, double (&t)[Sub
         c.ntiny += 1;
         if ((threadIdx.x & 63) == 0) __hip_atomic_fetch_add(c.tseq, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
         wait_flag<false>(c.tseq, c.ntiny * kSW);
-        const AtanhCoef ac = SUB_COEF(c);
+        const AtanhCoef ac = coef_load();  // scalar loads here, not 32 SGPRs held (cn_common.h)
 #pragma unroll
         for (int i = 0; i < K; ++i) {
             if (i < rc.CS) {
@@ -629,7 +624,7 @@ __device__ __forceinline__ void sub_body(SubCtx<Q> &c, int r, int m, double (&tc
 template <int Q>
 __global__ __launch_bounds__(64 * kSW, 1) void tile_sub_kernel(DevGraph g, DevState st, int max_iter, int nllr,
                                                                const int *__restrict__ col_idx,
-                                                               const int *__restrict__ row_ptr, AtanhCoef ac) {
+                                                               const int *__restrict__ row_ptr) {
     constexpr int F = SubCfg<Q>::F, K = SubCfg<Q>::K;
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     const SubLayout ly = sub_layout(g.k, g.m, F);
@@ -692,7 +687,6 @@ __global__ __launch_bounds__(64 * kSW, 1) void tile_sub_kernel(DevGraph g, DevSt
     c.p3dep = g.p3dep;
     c.ttab = LdsTanh{mlds.tanh};
     c.ltab = LdsAtanh{mlds.atanh};
-    c.ac = ac;
     c.k = g.k;
     c.wave = wave;
     c.j = j;
@@ -731,13 +725,13 @@ __global__ __launch_bounds__(64 * kSW, 1) void tile_sub_kernel(DevGraph g, DevSt
             double *sp = c.S + (size_t)col * F;
             const double Sj = *sp;
             *sp = 0.0;
-            const double chj = c.Cb[(size_t)col * kTile];
+            const double chj = *sub_c(c, col);
             const double Lj = chj + Sj;
             if (nllr) {
-                const double ap = c.first ? chj : ld_l2(c.Lb + (size_t)col * kTile);
+                const double ap = c.first ? chj : ld_l2(sub_l(c, col));
                 my_cnt += (fabs(Lj) <= 7.0 && ap * Lj < 0.0) ? 1 : 0;
             }
-            if (c.live) c.Lb[(size_t)col * kTile] = Lj;
+            if (c.live) *sub_l(c, col) = Lj;
             if (!(Lj < 0.0)) atomicOr(zb + (col >> 5) * F + f, 1u << (col & 31));
         }
         if (nllr && my_cnt) atomicAdd(cntl + f, my_cnt);
@@ -811,7 +805,7 @@ __global__ __launch_bounds__(64 * kSW, 1) void tile_sub_kernel(DevGraph g, DevSt
 template <int Q>
 __global__ __launch_bounds__(64 * kSW, 1) void tile_sub_stream_kernel(
     DevGraph g, DevState st, int max_iter, int nllr, const int *__restrict__ col_idx,
-    const int *__restrict__ row_ptr, AtanhCoef ac, uint64_t seed, int snr_point, double sigma, int64_t frame0,
+    const int *__restrict__ row_ptr, uint64_t seed, int snr_point, double sigma, int64_t frame0,
     int64_t total, unsigned long long *next, unsigned long long *ctr, int64_t handoff) {
     constexpr int F = SubCfg<Q>::F, K = SubCfg<Q>::K;
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
@@ -876,7 +870,6 @@ __global__ __launch_bounds__(64 * kSW, 1) void tile_sub_stream_kernel(
     c.p3dep = g.p3dep;
     c.ttab = LdsTanh{mlds.tanh};
     c.ltab = LdsAtanh{mlds.atanh};
-    c.ac = ac;
     c.k = g.k;
     c.wave = wave;
     c.j = j;
@@ -961,13 +954,13 @@ __global__ __launch_bounds__(64 * kSW, 1) void tile_sub_stream_kernel(
             double *sp = c.S + (size_t)col * F;
             const double Sj = *sp;
             *sp = 0.0;
-            const double chj = c.Cb[(size_t)col * kTile];
+            const double chj = *sub_c(c, col);
             const double Lj = chj + Sj;  // channel added after the sum (:173,185)
             if (nllr) {
-                const double ap = ld_l2(c.Lb + (size_t)col * kTile);  // previous L (= ch on a frame's first pass)
+                const double ap = ld_l2(sub_l(c, col));  // previous L (= ch on a frame's first pass)
                 my_cnt += (fabs(Lj) <= 7.0 && ap * Lj < 0.0) ? 1 : 0;
             }
-            if (c.live) c.Lb[(size_t)col * kTile] = Lj;
+            if (c.live) *sub_l(c, col) = Lj;
             if (!(Lj < 0.0)) atomicOr(zb + (col >> 5) * F + f, 1u << (col & 31));
         }
         if (nllr && my_cnt) atomicAdd(cntl + f, my_cnt);
@@ -1052,16 +1045,15 @@ hipError_t launch_tile_sub_stream(const DevGraph &g, const DevState &st, int max
         lds + 2 * 16 * sizeof(int) + 16 * sizeof(long long) + 16 > kSubLdsMax)
         return hipErrorInvalidValue;
     tile_sub_stream_kernel<4><<<st.ntiles * 4, 64 * kSW, lds, s>>>(g, st, max_iter, nllr ? 1 : 0, g.col_idx, g.row_ptr,
-                                                                   kAtanhCoef, seed, snr_point, sigma, frame0, total,
-                                                                   next, ctr, handoff);
+                                                                   seed, snr_point, sigma, frame0, total, next, ctr,
+                                                                   handoff);
     return hipGetLastError();
 }
 
 hipError_t launch_tile_sub(const DevGraph &g, const DevState &st, int max_iter, bool nllr, hipStream_t s) {
     const size_t lds = sub_lds_bytes(g);
     if (!lds || 2 * st.ntiles > st.nslots) return hipErrorInvalidValue;  // two rare-row buffers per workgroup
-    tile_sub_kernel<4><<<st.ntiles * 4, 64 * kSW, lds, s>>>(g, st, max_iter, nllr ? 1 : 0, g.col_idx, g.row_ptr,
-                                                            kAtanhCoef);
+    tile_sub_kernel<4><<<st.ntiles * 4, 64 * kSW, lds, s>>>(g, st, max_iter, nllr ? 1 : 0, g.col_idx, g.row_ptr);
     return hipGetLastError();
 }
 

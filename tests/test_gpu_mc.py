@@ -214,7 +214,13 @@ def test_stream_handoff_keeps_counters(gpu_available, monkeypatch, code, handoff
     a = dec.mc_run(SEED, sig, frames, 11, T, nllr=True)
     p = dec.profile_read()
     dec.profile(False)
-    assert p["tile"][1] == 2 and p["cn"][1] > 0, p  # the tail ran on the split path
+    assert p["tile"][1] == 2, p
+    # with 256 (every slot) the kernel hands off as soon as the supply is out,
+    # so the tail always runs; with 20 it runs only if some workgroup still
+    # holds a running frame when at most 20 are left -- timing-dependent (the
+    # last frames may all stop in the same pass), so only the counters are held
+    if handoff == "256":
+        assert p["cn"][1] > 0, p  # the tail ran on the split path
     monkeypatch.setenv("LDPC_HANDOFF", "0")
     b = dec.mc_run(SEED, sig, frames, 11, T, nllr=True)
     c = dec.mc_run(SEED, sig, frames, 11, T, nllr=True, static=True)
