@@ -652,14 +652,23 @@ def config5_extra(args, local, world, rank, dist):
         if cl:
             cn_bytes = 12.0 * H.nnz * int(loc[0, 6])
             tr, tsrc = committed_traffic(int(H.nnz), F, "phys_cn", snr)
+            # compaction makes launch shapes differ between runs: compare per frame-iteration
+            tfi = None
+            if tsrc:
+                tj = json.load(open(os.path.join(ROOT, tsrc)))
+                tfi = tj.get("traffic_bytes_per_frame_iteration")
             out["roofline"] = {"bound": "hbm", "kernel": "phys_cn_tile_kernel", "launches": cl,
                                "achieved": cn_bytes / (cms / 1e3) / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                                "frac": cn_bytes / (cms / 1e3) / 1e9 / HBM_PEAK_GBS,
                                "traffic": tr, "traffic_source": tsrc, "bytes_per_launch": cn_bytes / cl,
+                               "bytes_per_frame_iteration": 12.0 * H.nnz,
+                               "traffic_per_frame_iteration": tfi,
+                               "traffic_ratio": tfi / (12.0 * H.nnz) if tfi else None,
                                "bytes_model": "12 B x H edges x frame-iterations (L[col] gather + E_old read + "
                                               "E_new write, fp32), over the CN launches' HIP-event time; traffic = "
-                                              "committed PMC bytes per CN launch at this SNR (compare "
-                                              "bytes_per_launch)"}
+                                              "committed PMC bytes per CN launch at this SNR; "
+                                              "traffic_per_frame_iteration = those PMC bytes over the profiled "
+                                              "run's frame-iterations, vs bytes_per_frame_iteration (the model)"}
         return out
 
     out = {"what": "BASELINE config 5: DVB-S2 n=64800 r1/2 profile (seeded address table), physical mode "
@@ -981,6 +990,16 @@ def main():
         read_gbs = read_bytes / (decode_ms / 1e3) / 1e9 if decode_ms else 0.0
         out["roofline"]["read_achieved"] = read_gbs
         out["roofline"]["read_frac"] = read_gbs / HBM_PEAK_GBS
+        # ... and in bytes the fabric actually read: the committed PMC read bytes per frame-iteration
+        # (the same workload shape, tools/summarize_tile_profile.py) times this run's frame-iterations
+        tsrc = out["roofline"]["traffic_source"]
+        tj = json.load(open(os.path.join(ROOT, tsrc))) if tsrc else {}
+        fil = tj.get("frame_iterations_per_launch")
+        if fil and decode_ms:
+            rd_fi = tj["kernels"]["tile"]["read_bytes"] / fil
+            out["roofline"]["read_traffic_per_frame_iteration"] = rd_fi
+            out["roofline"]["read_traffic_achieved"] = rd_fi * local_iters / (decode_ms / 1e3) / 1e9
+            out["roofline"]["read_traffic_frac"] = out["roofline"]["read_traffic_achieved"] / HBM_PEAK_GBS
     if pgraph is not None:  # physical mode (not the reference's arithmetic: §8 f4)
         pnnz = int(pgraph.nnz)
         pms, pl = prof["phys"]

@@ -10,14 +10,21 @@ namespace ldpc {
 constexpr float kPhiMin = 1.0e-7f;  // phi(1e-7) ~ 16.8: caps the magnitude
 constexpr float kPhiMax = 30.0f;    // phi(30) ~ 1.9e-13
 
-// phi(x) = log((e^x + 1)/(e^x - 1)) with the hardware v_exp_f32 / v_log_f32 /
-// v_rcp_f32 (one instruction each).  Below x = 2^-5 the quotient loses bits to
-// e^x - 1, so use the series phi(x) ~ log(2/x) + x^2/12 there.
+// phi(x) = log((e^x + 1)/(e^x - 1)) straight on the hardware transcendentals
+// v_exp_f32 (2^x), v_rcp_f32 and v_log_f32 (log2), one instruction each: the
+// clamped x keeps every operand normal (t = e^x in [1.03, 1.1e13], the
+// quotient in [1, 65]), so none of the denormal / correct-rounding wrappers
+// of __expf, __frcp_rn and __logf is needed (they made phi ~30 VALU; the
+// physical mode is our fp32 design, checked against its CPU restatement by
+// decisions, tests/test_phys.py).  Below x = 2^-5 the quotient loses bits to
+// e^x - 1, so there phi ~ log(2/x) + x^2/12 = ln2 (1 - log2 x) + x^2/12.
 __device__ __forceinline__ float phi(float x) {
+    constexpr float kLn2 = 0.693147180559945309f, kLog2e = 1.442695040888963407f;
     x = fminf(fmaxf(x, kPhiMin), kPhiMax);
-    if (x < 0.03125f) return __logf(2.0f * __frcp_rn(x)) + x * x * (1.0f / 12.0f);
-    const float t = __expf(x);
-    return __logf((t + 1.0f) * __frcp_rn(t - 1.0f));
+    const float t = __builtin_amdgcn_exp2f(x * kLog2e);
+    const float big = __builtin_amdgcn_logf((t + 1.0f) * __builtin_amdgcn_rcpf(t - 1.0f)) * kLn2;
+    const float small = (1.0f - __builtin_amdgcn_logf(x)) * kLn2 + x * x * (1.0f / 12.0f);
+    return x < 0.03125f ? small : big;
 }
 
 }  // namespace ldpc

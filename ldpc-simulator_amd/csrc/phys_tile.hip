@@ -50,6 +50,7 @@ __device__ __forceinline__ void st_e32(float *p, float v) { __builtin_nontempora
 
 constexpr int kRowsPerWave = 4;
 constexpr int kColsPerWave = 8;
+constexpr int kVnBatch = 4;  // columns per batch of phys_vn_tile's batched loads (2 / 8: same or slower)
 
 __device__ __forceinline__ int uniform(int x) { return __builtin_amdgcn_readfirstlane(x); }
 
@@ -88,6 +89,47 @@ __global__ void phys_tile_init_kernel(DevGraph g, DevState st, PhysTile pt, int 
     }
 }
 
+// One row's update from its gathered posteriors Lc and messages Eo (E_old;
+// unused on iteration 0, for a stopped frame or in the syndrome-only sweep):
+// phi(|M|) and the signs in registers, E_new = sign * phi(S - phi(|M_i|)).
+// Returns the row parity of the hard decisions (L < 0).
+template <int kDeg>
+__device__ __forceinline__ uint32_t phys_row(float *__restrict__ Et, int beg, int deg, const float (&Lc)[kDeg],
+                                             const float (&Eo)[kDeg], bool first, bool live, bool syn_only) {
+    uint32_t hp = 0u, sg = 0u;
+    float ph[kDeg];
+    float S = 0.0f;
+#pragma unroll
+    for (int i = 0; i < kDeg; ++i) {
+        if (i < deg) {
+            hp ^= Lc[i] < 0.0f ? 1u : 0u;
+            if (!syn_only) {
+                const float M = (first || !live) ? Lc[i] : Lc[i] - Eo[i];
+                ph[i] = phi(fabsf(M));
+                S += ph[i];
+                sg |= (M < 0.0f ? 1u : 0u) << i;
+            }
+        }
+    }
+    if (!syn_only && live) {
+        const uint32_t neg = __popc(sg) & 1u;
+#pragma unroll
+        for (int i = 0; i < kDeg; ++i) {
+            if (i < deg) {
+                const float mag = phi(fmaxf(S - ph[i], 0.0f));
+                st_e32(&Et[(beg + i) * kTile], ((neg ^ (sg >> i)) & 1u) ? -mag : mag);
+            }
+        }
+    }
+    return hp;
+}
+
+// A wavefront takes kRowsPerWave rows of one tile, one after the other: rows
+// of degree <= kDeg with their gathers and E_old loads issued together
+// (phys_row), longer rows in two sweeps with M recomputed (same values).
+// (Batching the loads of 2 or 4 rows before any row's math measured 1.5-3 %
+// slower once phi was cheap: the extra registers cost occupancy,
+// profiles/r6_ab/r6e_c5.)
 template <int kDeg>
 __global__ __launch_bounds__(256) void phys_cn_tile_kernel(DevGraph g, DevState st, PhysTile pt, int it,
                                                            int syn_only, int per_tile, int items,
@@ -104,45 +146,30 @@ __global__ __launch_bounds__(256) void phys_cn_tile_kernel(DevGraph g, DevState 
     const float *Lt = pt.L + (size_t)tile * g.n * kTile + lane;
     float *Et = pt.E + (size_t)tile * g.nnz * kTile + lane;
     const bool first = it == 0;
-    const bool upd = !syn_only && live;
+    const bool readE = !first && !syn_only && live;
     uint32_t bad = 0u;
     const int r0 = (part * 4 + wave) * kRowsPerWave;
     for (int rr = 0; rr < kRowsPerWave; ++rr) {
         const int r = r0 + rr;
         if (r >= g.m) break;
-        const int beg = row_ptr[r], end = row_ptr[r + 1], deg = end - beg;
-        if (deg == 0) continue;
-        uint32_t hp = 0u;
+        const int beg = row_ptr[r], deg = row_ptr[r + 1] - beg;
         if (deg <= kDeg) {
-            float ph[kDeg];
-            uint32_t sg = 0u;
-            float S = 0.0f;
+            float Lc[kDeg], Eo[kDeg];
+            // lane-masked loads: a tile with few running frames moves only
+            // their sectors, not 256 B per wavefront access
 #pragma unroll
             for (int i = 0; i < kDeg; ++i) {
+                Lc[i] = 0.0f;
+                Eo[i] = 0.0f;
                 if (i < deg) {
-                    // lane-masked loads: a tile with few running frames moves
-                    // only their sectors, not 256 B per wavefront access
-                    const float Lc = live ? Lt[col_idx[beg + i] * kTile] : 0.0f;
-                    hp ^= Lc < 0.0f ? 1u : 0u;
-                    if (!syn_only) {
-                        const float M = (first || !live) ? Lc : Lc - ld_e32(&Et[(beg + i) * kTile]);
-                        ph[i] = phi(fabsf(M));
-                        S += ph[i];
-                        sg |= (M < 0.0f ? 1u : 0u) << i;
-                    }
+                    if (live) Lc[i] = Lt[col_idx[beg + i] * kTile];
+                    if (readE) Eo[i] = ld_e32(&Et[(beg + i) * kTile]);
                 }
             }
-            if (upd) {
-                const uint32_t neg = __popc(sg) & 1u;
-#pragma unroll
-                for (int i = 0; i < kDeg; ++i) {
-                    if (i < deg) {
-                        const float mag = phi(fmaxf(S - ph[i], 0.0f));
-                        st_e32(&Et[(beg + i) * kTile], ((neg ^ (sg >> i)) & 1u) ? -mag : mag);
-                    }
-                }
-            }
-        } else {  // long row: two sweeps, M recomputed (same values)
+            bad |= phys_row<kDeg>(Et, beg, deg, Lc, Eo, first, live, syn_only != 0);
+        } else {
+            const int end = beg + deg;
+            uint32_t hp = 0u;
             float S = 0.0f;
             uint32_t neg = 0u;
             for (int e = beg; e < end; ++e) {
@@ -154,7 +181,7 @@ __global__ __launch_bounds__(256) void phys_cn_tile_kernel(DevGraph g, DevState 
                     neg ^= (M < 0.0f) ? 1u : 0u;
                 }
             }
-            if (upd) {
+            if (!syn_only && live) {
                 for (int e = beg; e < end; ++e) {
                     const float Lc = Lt[col_idx[e] * kTile];
                     const float M = first ? Lc : Lc - ld_e32(&Et[e * kTile]);
@@ -162,14 +189,20 @@ __global__ __launch_bounds__(256) void phys_cn_tile_kernel(DevGraph g, DevState 
                     st_e32(&Et[e * kTile], ((neg ^ ((M < 0.0f) ? 1u : 0u)) != 0u) ? -mag : mag);
                 }
             }
+            bad |= hp;
         }
-        bad |= hp;
     }
     // syndrome of the posterior of iteration it-1 (none before iteration 0)
     if (it >= 1 && live && bad) pt.bad[(it & 1) * pt.cap + f] = 1;
     }
 }
 
+// A wavefront takes kColsPerWave columns of one tile: L = Lambda + E_0 + E_1
+// + ... in CSC order.  With every column of degree <= kCD (template; 0 = the
+// plain loop for any degree), all the wavefront's message loads -- up to
+// 8 x kCD -- are issued before the first sum (the per-column loop waited one
+// memory latency per message: each add needs its load).
+template <int kCD>
 __global__ __launch_bounds__(256) void phys_vn_tile_kernel(DevGraph g, DevState st, PhysTile pt, int it,
                                                            int per_tile, int items, const int *__restrict__ csc_ptr,
                                                            const int *__restrict__ csc_edge, int *active_count,
@@ -192,15 +225,52 @@ __global__ __launch_bounds__(256) void phys_vn_tile_kernel(DevGraph g, DevState 
         const int j0 = (part * 4 + wave) * kColsPerWave;
         const int j1 = min(g.n, j0 + kColsPerWave);
         uint32_t hb = 0u;  // this lane's hard decisions of the 8 columns (early syndrome)
-        for (int j = j0; j < j1; ++j) {
-            if (upd) {  // lane-masked: converged / finished frames move no data
-                float s = Lamt[j * kTile];
-                for (int p = csc_ptr[j]; p < csc_ptr[j + 1]; ++p) s += ld_e32(&Et[csc_edge[p] * kTile]);
-                Lt[j * kTile] = s;
-                hb |= (s < 0.0f ? 1u : 0u) << (j - j0);
+        if constexpr (kCD > 0) {
+            // batches of CB columns (CB x kCD loads in flight; more batch
+            // columns spill the uniform edge indices)
+            constexpr int CB = kVnBatch;
+#pragma unroll
+            for (int b = 0; b < kColsPerWave / CB; ++b) {
+                float Ev[CB][kCD], La[CB];
+                int p0[CB], cd[CB];
+#pragma unroll
+                for (int q = 0; q < CB; ++q) {
+                    const int j = j0 + b * CB + q;
+                    p0[q] = j < j1 ? csc_ptr[j] : 0;
+                    cd[q] = j < j1 ? csc_ptr[j + 1] - p0[q] : 0;
+                }
+                // lane-masked: converged / finished frames move no data
+#pragma unroll
+                for (int q = 0; q < CB; ++q) {
+                    La[q] = 0.0f;
+                    if (upd && cd[q] > 0) La[q] = Lamt[(j0 + b * CB + q) * kTile];
+#pragma unroll
+                    for (int i = 0; i < kCD; ++i) {
+                        Ev[q][i] = 0.0f;
+                        if (upd && i < cd[q]) Ev[q][i] = ld_e32(&Et[csc_edge[p0[q] + i] * kTile]);
+                    }
+                }
+#pragma unroll
+                for (int q = 0; q < CB; ++q) {
+                    float sum = La[q];
+#pragma unroll
+                    for (int i = 0; i < kCD; ++i)
+                        if (i < cd[q]) sum += Ev[q][i];
+                    if (upd && j0 + b * CB + q < j1) Lt[(j0 + b * CB + q) * kTile] = sum;
+                    hb |= (sum < 0.0f ? 1u : 0u) << (b * CB + q);
+                }
+            }
+        } else {
+            for (int j = j0; j < j1; ++j) {
+                if (upd) {
+                    float sum = Lamt[j * kTile];
+                    for (int p = csc_ptr[j]; p < csc_ptr[j + 1]; ++p) sum += ld_e32(&Et[csc_edge[p] * kTile]);
+                    Lt[j * kTile] = sum;
+                    hb |= (sum < 0.0f ? 1u : 0u) << (j - j0);
+                }
             }
         }
-        if (j0 < g.n) pt.zb[((size_t)tile * ((g.n + 7) >> 3) + (j0 >> 3)) * kTile + lane] = (uint8_t)hb;
+        if (j0 < g.n && upd) pt.zb[((size_t)tile * ((g.n + 7) >> 3) + (j0 >> 3)) * kTile + lane] = (uint8_t)hb;
     }
     if (part == 0 && wave == 0) {
         if (conv_now) {  // syndrome of iteration it-1 was zero
@@ -424,8 +494,12 @@ hipError_t launch_phys_tile_vn(const DevGraph &g, const DevState &st, const Phys
                                int max_iter, hipStream_t s) {
     const int per_tile = (g.n + 4 * kColsPerWave - 1) / (4 * kColsPerWave);
     const int items = (int)xcd_items(st.ntiles, per_tile);
-    phys_vn_tile_kernel<<<stride_grid(items), 256, 0, s>>>(g, st, pt, it, per_tile, items, g.csc_ptr, g.csc_edge,
-                                                           active_count, max_iter);
+    if (g.max_col_deg <= 8)
+        phys_vn_tile_kernel<8><<<stride_grid(items), 256, 0, s>>>(g, st, pt, it, per_tile, items, g.csc_ptr,
+                                                                  g.csc_edge, active_count, max_iter);
+    else
+        phys_vn_tile_kernel<0><<<stride_grid(items), 256, 0, s>>>(g, st, pt, it, per_tile, items, g.csc_ptr,
+                                                                  g.csc_edge, active_count, max_iter);
     return hipGetLastError();
 }
 

@@ -13,7 +13,8 @@
 #include <stdlib.h>
 #include <string.h>
 
-/* same formula as the GPU's default (hardware exp/log) path */
+/* the GPU evaluates the same formula on the hardware exp2 / rcp / log2 (phys_math.h):
+   equal to this one to a few ulp, so tests compare decisions */
 static float phi(float x) {
     x = fminf(fmaxf(x, 1.0e-7f), 30.0f);
     if (x < 0.03125f) return logf(2.0f * (1.0f / x)) + x * x * (1.0f / 12.0f);

@@ -58,6 +58,9 @@ def main(src, dst):
         out = {"code": "dvbs2_profile_64800_0.5", "snr_db": float(snr), "frames": 8192, "edges": EDGES,
                "fetch_correction_factor": factor, "factor_source": vn,
                "frame_iterations": fi, "alg_bytes_per_launch": 12.0 * EDGES * fi / calls_cn if fi else None,
+               # per frame-iteration (launch shapes differ under compaction, frame-iterations do not)
+               "model_bytes_per_frame_iteration": 12.0 * EDGES,
+               "traffic_bytes_per_frame_iteration": (rd + wr) * calls_cn / fi if fi else None,
                "kernels": {"phys_cn": {"kernel": cn, "read_bytes": rd, "write_bytes": wr, "traffic_bytes": rd + wr,
                                        "avg_ns": float(s["AverageNs"]), "calls": int(s["Calls"]),
                                        "traffic_GBs": (rd + wr) / float(s["AverageNs"])}}}

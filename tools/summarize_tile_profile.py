@@ -45,7 +45,13 @@ def main(src, dst, nnz, frames):
     st = next(v for n, v in stats.items() if is_tile(n))
     rd = fetch[tk][0] * 1024.0 * factor
     wr = write[tk][0] * 1024.0
+    # frame-iterations one tile launch decoded (the traced bench line: one launch per step decodes
+    # its `frames` frames, avg_iters each) -> bench.py scales the PMC bytes to its own run
+    log = open(os.path.join(src, "bench_trace.log")).read()
+    js = json.loads(log[log.index("{\"metric\""):].split("\n")[0])
+    fi_launch = js["avg_iters"] * frames
     out = {"fetch_correction_factor": factor, "factor_source": vn, "frames": frames, "edges": nnz,
+           "frame_iterations_per_launch": fi_launch,
            "kernels": {"tile": {"kernel": tk, "read_bytes": rd, "write_bytes": wr, "traffic_bytes": rd + wr,
                                 "avg_ns": float(st["AverageNs"]), "calls": int(st["Calls"]),
                                 "traffic_GBs": (rd + wr) / float(st["AverageNs"])}}}
