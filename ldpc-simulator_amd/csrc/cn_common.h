@@ -83,6 +83,13 @@ __device__ __forceinline__ double cn_tanh(double M, const LdsTanh &t) { return c
 // kernel argument (or hoisted) they would hold 32 SGPRs for the whole kernel,
 // which in the row-pipeline decoders spills other uniforms into VGPR lanes and
 // reloads them with v_readlane in the loop.
+// The streaming tile kernels run atanh_f on most rows at 2-3 dB, where the
+// loads (and their lgkmcnt waits, shared with LDS) cost more than the held
+// SGPRs: they take the coefficients as a kernel argument (kStreamCoefArg).
+#ifndef LDPC_STREAM_COEF_ARG
+#define LDPC_STREAM_COEF_ARG 1
+#endif
+constexpr bool kStreamCoefArg = LDPC_STREAM_COEF_ARG != 0;
 static __constant__ AtanhCoef kAtanhCoefK = kAtanhCoef;
 typedef __attribute__((address_space(4))) const AtanhCoef ConstCoef;
 __device__ __forceinline__ AtanhCoef coef_load() {

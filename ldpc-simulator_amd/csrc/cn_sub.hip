@@ -165,16 +165,35 @@ __global__ __launch_bounds__(64 * W, WPS) void cn_sub_kernel(DevGraph g, DevStat
     const double P = chain[f];
     // q = P/t (div_nr where exact, cn_common.h); E_new = 2 atanh(clip(q)), or
     // 2q when every quotient of the wavefront is below 2^-27 (spa_math.h
-    // kAtanhIdent), slot by slot; frame-less lanes do not vote
+    // kAtanhIdent), slot by slot; frame-less lanes do not vote.
+    // Saturated rows (the streaming tail at 2.5-3 dB: the frames that fail
+    // there have 85-97 % of their t at +-CL) give most slots of a lane one
+    // quotient magnitude: a slot where every live lane's |q| equals its slot-0
+    // |q| takes slot 0's E_new with its own sign -- atanh_f(clip_cl(q)) is odd
+    // bit for bit and 2q trivially so (tests/test_math.py), so this is the
+    // same value, one atanh per lane and row instead of one per slot
+    // (tile8.hip's memo).  Lanes that do not vote keep values nothing stores.
     const double lim = live ? kAtanhIdent : INFINITY;
-    auto en = [&](double q) {
-        return __ballot(!(fabs(q) < lim)) == 0ull ? 2.0 * q : 2.0 * atanh_f(clip_cl(q), ltab, ac);
+    double key = 0.0, E0 = 0.0;
+    auto en = [&](int i, double q) {
+        double En;
+        if (__ballot(!(fabs(q) < lim)) == 0ull)
+            En = 2.0 * q;
+        else if (i > 0 && __ballot(live && i < nj && fabs(q) != key) == 0ull)
+            En = dfrom((dbits(E0) & 0x7fffffffffffffffull) | (dbits(q) & 0x8000000000000000ull));
+        else
+            En = 2.0 * atanh_f(clip_cl(q), ltab, ac);
+        if (i == 0) {
+            key = fabs(q);
+            E0 = En;
+        }
+        return En;
     };
     if (div_nr_ok(live ? P : 1.0)) {
 #pragma unroll
         for (int i = 0; i < K; ++i) {
             if (i < CS) {  // wave-uniform
-                const double En = en(div_nr(P, t[i]));
+                const double En = en(i, div_nr(P, t[i]));
                 if (live && i < nj) cs_st_e(&Et[(size_t)(e0 + i) * g.ef], En);
             }
         }
@@ -183,7 +202,7 @@ __global__ __launch_bounds__(64 * W, WPS) void cn_sub_kernel(DevGraph g, DevStat
 #pragma unroll
     for (int i = 0; i < K; ++i) {
         if (i < CS) {
-            const double En = en(P / t[i]);
+            const double En = en(i, P / t[i]);
             if (live && i < nj) cs_st_e(&Et[(size_t)(e0 + i) * g.ef], En);
         }
     }

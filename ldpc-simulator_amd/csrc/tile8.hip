@@ -173,6 +173,8 @@ struct T8Ctx {
     int *flag, *tinyf, *tseq, *p3row;
     LdsTanh ttab;
     LdsAtanh ltab;
+    AtanhCoef ac;   // kernel-argument coefficients (when coef_arg)
+    bool coef_arg;  // P3 uses ac instead of coef_load() (compile-time per kernel)
     int m, k, wave, j, f, nnz;
     int h;  // pair form: this lane's row of the pair (lane = h*32 + j*8 + f); 0 otherwise
     int ep0;
@@ -412,7 +414,7 @@ __device__ __forceinline__ void t8_p3(T8Ctx<K> &c, int r, double (&t)[K]) {
     T8_STAMP(q1);
     T8_ADD(c, 2, q0, q1);
     const bool tiny_row = uniform(lds_ld(c.tinyf + s)) != 0;
-    const AtanhCoef ac = coef_load();  // scalar loads for this P3 only, not 32 SGPRs held (cn_common.h)
+    const AtanhCoef ac = c.coef_arg ? c.ac : coef_load();  // scalar loads for this P3 only (cn_common.h)
     const int nj = t8_nj(c, rc);
     const double tI = c.slot[(kSR8 + s) * kF8];
     const double P = c.slot[s * kF8] * tI;  // (t_0 * ... * t_{deg-2}) * t_id: left to right (:151-152)
@@ -812,7 +814,7 @@ __device__ __forceinline__ void tp_p3(T8Ctx<K> &c, int q, double (&t)[K], TpStag
     T8_STAMP(q1);
     T8_ADD(c, 2, q0, q1);
     const bool tiny_row = lds_ld(c.tinyf + s * 2 + c.h) != 0;
-    const AtanhCoef ac = coef_load();  // scalar loads for this P3 only (cn_common.h)
+    const AtanhCoef ac = c.coef_arg ? c.ac : coef_load();  // scalar loads for this P3 only (cn_common.h)
     const bool tiny_any = __ballot(tiny_row) != 0ull;
     const int nj = tp_nj(c, rc);
     const double tI = c.slot[(c.ns + s * 2 + c.h) * kF8];
@@ -1130,6 +1132,7 @@ __global__ __launch_bounds__(64 * kW8, 1) void tile8_kernel(DevGraph g, DevState
 
     T8Ctx<K> c;
     t8_setup<K, LA, PAIR, NS>(c, lds, ly, g, st, tile, sub, col_idx, row_ptr);
+    c.coef_arg = false;  // the static decoder loads them
     c.R = t8_ring(PAIR, D);
     // the identity edge's wavefront: with D = 3 wavefront 0, which otherwise
     // waits longest for the chain; with D = 2 the last one (wavefront 0's
@@ -1220,7 +1223,7 @@ __global__ __launch_bounds__(64 * kW8, 1) void tile8_kernel(DevGraph g, DevState
 template <int K, bool LA, int D, bool PAIR = false>
 __global__ __launch_bounds__(64 * kW8, 1) void tile8_stream_kernel(
     DevGraph g, DevState st, int max_iter, int nllr, const int *__restrict__ col_idx,
-    const int *__restrict__ row_ptr, uint64_t seed, int snr_point, double sigma, int64_t frame0,
+    const int *__restrict__ row_ptr, AtanhCoef ac, uint64_t seed, int snr_point, double sigma, int64_t frame0,
     int64_t total, unsigned long long *next, unsigned long long *ctr, int64_t handoff) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     __shared__ long long gidx[kF8];  // refill: slot f's new frame index (< 0: none)
@@ -1256,6 +1259,8 @@ __global__ __launch_bounds__(64 * kW8, 1) void tile8_stream_kernel(
 
     T8Ctx<K> c;
     t8_setup<K, LA, PAIR, NS>(c, lds, ly, g, st, tile, sub, col_idx, row_ptr);
+    c.coef_arg = kStreamCoefArg;
+    c.ac = ac;
     c.R = t8_ring(PAIR, D);
     c.idwave = 0;  // as tile8_kernel
     const int m = g.m;
@@ -1444,17 +1449,17 @@ hipError_t launch_tile8_stream(const DevGraph &g, const DevState &st, int max_it
     switch (t8_variant(g)) {
         case 121:
             tile8_stream_kernel<10, true, 2, true><<<grid, block, lds, s>>>(g, st, max_iter, nllr ? 1 : 0, g.col_idx,
-                                                                         g.row_ptr, seed, snr_point,
+                                                                         g.row_ptr, kAtanhCoef, seed, snr_point,
                                                                          sigma, frame0, total, next, ctr, handoff);
             break;
         case 11:
             tile8_stream_kernel<5, true, kD5><<<grid, block, lds, s>>>(g, st, max_iter, nllr ? 1 : 0, g.col_idx,
-                                                                      g.row_ptr, seed, snr_point, sigma,
+                                                                      g.row_ptr, kAtanhCoef, seed, snr_point, sigma,
                                                                       frame0, total, next, ctr, handoff);
             break;
         case 16:
             tile8_stream_kernel<8, false, kD8><<<grid, block, lds, s>>>(g, st, max_iter, nllr ? 1 : 0, g.col_idx,
-                                                                       g.row_ptr, seed, snr_point, sigma,
+                                                                       g.row_ptr, kAtanhCoef, seed, snr_point, sigma,
                                                                        frame0, total, next, ctr, handoff);
             break;
         default:

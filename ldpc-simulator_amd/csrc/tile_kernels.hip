@@ -133,6 +133,8 @@ struct TileCtx {
     int *flag, *tinyf, *tseq;
     LdsTanh ttab;
     LdsAtanh ltab;
+    AtanhCoef ac;   // kernel-argument coefficients (when coef_arg)
+    bool coef_arg;  // P3 uses ac instead of coef_load() (compile-time per kernel)
     int k, wave;
     uint32_t lane;
     int ep0;  // epoch of row 0 in this pass (flags are tagged (epoch, stage))
@@ -232,7 +234,7 @@ __device__ __forceinline__ void tile_p3(TileCtx &c, int r, double (&t)[kTK]) {
     wait_flag(c.flag + s, ep + kTW);
     const double P = c.slot[s * kTile + c.lane];
     const bool tiny_row = uniform(lds_ld(c.tinyf + s)) != 0;
-    const AtanhCoef ac = coef_load();  // scalar loads for this P3 only (cn_common.h)
+    const AtanhCoef ac = c.coef_arg ? c.ac : coef_load();  // scalar loads for this P3 only (cn_common.h)
     if (!tiny_row) {
 #pragma unroll
         for (int i = 0; i < kTK; ++i)
@@ -418,6 +420,7 @@ __global__ __launch_bounds__(64 * kTW, 1) void tile_kernel(DevGraph g, DevState 
     c.tseq = flags + 2 * kTR;
     c.ttab = LdsTanh{mlds.tanh};
     c.ltab = LdsAtanh{mlds.atanh};
+    c.coef_arg = false;  // the static decoder loads them
     c.k = g.k;
     c.lane = lane;
     c.wave = wave;
@@ -502,7 +505,7 @@ __device__ __forceinline__ bool tile_refill(const DevState &st, int lane, bool w
 
 __global__ __launch_bounds__(64 * kTW, 1) void tile_stream_kernel(DevGraph g, DevState st, int max_iter, int nllr,
                                                                   const int *__restrict__ col_idx,
-                                                                  const int *__restrict__ row_ptr,
+                                                                  const int *__restrict__ row_ptr, AtanhCoef ac,
                                                                   uint64_t seed, int snr_point, double sigma,
                                                                   int64_t frame0, int64_t total,
                                                                   unsigned long long *next,
@@ -555,6 +558,8 @@ __global__ __launch_bounds__(64 * kTW, 1) void tile_stream_kernel(DevGraph g, De
     c.tseq = flags + 2 * kTR;
     c.ttab = LdsTanh{mlds.tanh};
     c.ltab = LdsAtanh{mlds.atanh};
+    c.coef_arg = kStreamCoefArg;
+    c.ac = ac;
     c.k = g.k;
     c.lane = lane;
     c.wave = wave;
@@ -742,7 +747,7 @@ hipError_t launch_tile_stream(const DevGraph &g, const DevState &st, int max_ite
                                       handoff, s);
     if (!lds || !g.a_packed || !st.ubits || 2 * st.ntiles > st.nslots) return hipErrorInvalidValue;
     tile_stream_kernel<<<st.ntiles, 64 * kTW, lds, s>>>(g, st, max_iter, nllr ? 1 : 0, g.col_idx, g.row_ptr,
-                                                        seed, snr_point, sigma, frame0, total, next, ctr);
+                                                        kAtanhCoef, seed, snr_point, sigma, frame0, total, next, ctr);
     return hipGetLastError();
 }
 

@@ -195,6 +195,8 @@ struct SubCtx {
     const int *p3dep;
     LdsTanh ttab;
     LdsAtanh ltab;
+    AtanhCoef ac;   // kernel-argument coefficients (when coef_arg)
+    bool coef_arg;  // P3 uses ac instead of coef_load() (compile-time per kernel)
     // uniform (SGPR) tile bases + this lane's byte offset: every access is a
     // 32-bit per-lane offset from a scalar base (global_load ... v_off, s_base)
     const char *Eu, *Lu, *Cu;
@@ -498,7 +500,7 @@ __device__ __forceinline__ void sub_p3_body(SubCtx<Q> &c, int r, double (&t)[Sub
             for (int i = 0; i < K; ++i)
                 if (i < rc.CS) t[i] = 2.0 * t[i];
         } else {
-            const AtanhCoef ac = coef_load();  // scalar loads here, not 32 SGPRs held (cn_common.h)
+            const AtanhCoef ac = c.coef_arg ? c.ac : coef_load();  // scalar loads here (cn_common.h)
 #pragma unroll
             for (int i = 0; i < K; ++i)
                 if (i < rc.CS) t[i] = 2.0 * atanh_f(clip_cl(t[i]), c.ltab, ac);
@@ -515,7 +517,7 @@ __device__ __forceinline__ void sub_p3_body(SubCtx<Q> &c, int r, double (&t)[Sub
         c.ntiny += 1;
         if ((threadIdx.x & 63) == 0) __hip_atomic_fetch_add(c.tseq, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
         wait_flag<false>(c.tseq, c.ntiny * kSW);
-        const AtanhCoef ac = coef_load();  // scalar loads here, not 32 SGPRs held (cn_common.h)
+        const AtanhCoef ac = c.coef_arg ? c.ac : coef_load();  // scalar loads here (cn_common.h)
 #pragma unroll
         for (int i = 0; i < K; ++i) {
             if (i < rc.CS) {
@@ -624,7 +626,7 @@ __device__ __forceinline__ void sub_body(SubCtx<Q> &c, int r, int m, double (&tc
 template <int Q>
 __global__ __launch_bounds__(64 * kSW, 1) void tile_sub_kernel(DevGraph g, DevState st, int max_iter, int nllr,
                                                                const int *__restrict__ col_idx,
-                                                               const int *__restrict__ row_ptr) {
+                                                               const int *__restrict__ row_ptr, AtanhCoef ac) {
     constexpr int F = SubCfg<Q>::F, K = SubCfg<Q>::K;
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     const SubLayout ly = sub_layout(g.k, g.m, F);
@@ -687,6 +689,8 @@ __global__ __launch_bounds__(64 * kSW, 1) void tile_sub_kernel(DevGraph g, DevSt
     c.p3dep = g.p3dep;
     c.ttab = LdsTanh{mlds.tanh};
     c.ltab = LdsAtanh{mlds.atanh};
+    c.coef_arg = false;  // the static decoder loads them (1 dB: atanh on few rows)
+    c.ac = ac;
     c.k = g.k;
     c.wave = wave;
     c.j = j;
@@ -805,7 +809,7 @@ __global__ __launch_bounds__(64 * kSW, 1) void tile_sub_kernel(DevGraph g, DevSt
 template <int Q>
 __global__ __launch_bounds__(64 * kSW, 1) void tile_sub_stream_kernel(
     DevGraph g, DevState st, int max_iter, int nllr, const int *__restrict__ col_idx,
-    const int *__restrict__ row_ptr, uint64_t seed, int snr_point, double sigma, int64_t frame0,
+    const int *__restrict__ row_ptr, AtanhCoef ac, uint64_t seed, int snr_point, double sigma, int64_t frame0,
     int64_t total, unsigned long long *next, unsigned long long *ctr, int64_t handoff) {
     constexpr int F = SubCfg<Q>::F, K = SubCfg<Q>::K;
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
@@ -870,6 +874,8 @@ __global__ __launch_bounds__(64 * kSW, 1) void tile_sub_stream_kernel(
     c.p3dep = g.p3dep;
     c.ttab = LdsTanh{mlds.tanh};
     c.ltab = LdsAtanh{mlds.atanh};
+    c.coef_arg = kStreamCoefArg;
+    c.ac = ac;
     c.k = g.k;
     c.wave = wave;
     c.j = j;
@@ -1045,15 +1051,16 @@ hipError_t launch_tile_sub_stream(const DevGraph &g, const DevState &st, int max
         lds + 2 * 16 * sizeof(int) + 16 * sizeof(long long) + 16 > kSubLdsMax)
         return hipErrorInvalidValue;
     tile_sub_stream_kernel<4><<<st.ntiles * 4, 64 * kSW, lds, s>>>(g, st, max_iter, nllr ? 1 : 0, g.col_idx, g.row_ptr,
-                                                                   seed, snr_point, sigma, frame0, total, next, ctr,
-                                                                   handoff);
+                                                                   kAtanhCoef, seed, snr_point, sigma, frame0, total,
+                                                                   next, ctr, handoff);
     return hipGetLastError();
 }
 
 hipError_t launch_tile_sub(const DevGraph &g, const DevState &st, int max_iter, bool nllr, hipStream_t s) {
     const size_t lds = sub_lds_bytes(g);
     if (!lds || 2 * st.ntiles > st.nslots) return hipErrorInvalidValue;  // two rare-row buffers per workgroup
-    tile_sub_kernel<4><<<st.ntiles * 4, 64 * kSW, lds, s>>>(g, st, max_iter, nllr ? 1 : 0, g.col_idx, g.row_ptr);
+    tile_sub_kernel<4><<<st.ntiles * 4, 64 * kSW, lds, s>>>(g, st, max_iter, nllr ? 1 : 0, g.col_idx, g.row_ptr,
+                                                            kAtanhCoef);
     return hipGetLastError();
 }
 
