@@ -43,3 +43,25 @@ def test_ber_curve_overlays_reference_north_star_code(gpu_available):
         assert r["ber_lo"] <= r["ber_ref"] <= r["ber_hi"], r
     fers = [r["fer_gpu"] for r in rows]
     assert all(a > b for a, b in zip(fers, fers[1:])), fers
+
+
+def test_ber_curve_overlays_reference_config4_code(gpu_available):
+    """The same overlay on wimax_2304_0.75A (BASELINE config 4's code) at
+    2.0 / 2.5 / 3.0 dB, where its FER moves (0.8 -> 0.07), against the
+    reference's own main.py run (tests/golden/gen_ber_curve.py --code
+    wimax_2304_0.75A: 48 / 64 / 96 frames).  Its failing frames at 3 dB carry
+    few or no information-bit errors (the sign quirk of odd-degree rows,
+    DESIGN.md §2), in the reference and on the GPU alike."""
+    import ber_overlay
+    from conftest import hstd_for
+    from ldpc_amd.device import Decoder, Graph
+
+    dec = Decoder(Graph(hstd_for("wimax_2304_0.75A"), device=0), 9600)
+    rows = ber_overlay.overlay(dec, groups=200, code="wimax_2304_0.75A")
+    assert [r["snr_db"] for r in rows] == [2.0, 2.5, 3.0]
+    for r in rows:
+        print(r)
+        assert r["fer_lo"] <= r["fer_ref"] <= r["fer_hi"], r
+        assert r["ber_lo"] <= r["ber_ref"] <= r["ber_hi"], r
+    fers = [r["fer_gpu"] for r in rows]
+    assert all(a > b for a, b in zip(fers, fers[1:])), fers
