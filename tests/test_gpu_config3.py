@@ -81,3 +81,45 @@ def test_three_point_call_equals_oracle(gpu_available):
     # the streaming schedule (ldpc_mc_run's default, bench's extra SNR points) agrees
     stream = dec.mc_run(SEED, sig, B, frame0, T)
     np.testing.assert_array_equal(stream, ctr)
+
+
+def test_bench_3db_point_shape(gpu_available):
+    """The bench's whole 3 dB point at its real shape: 262,144 frames of
+    wimax_2304_0.5 streamed through 8,192 slots in ONE mc_run (supply order,
+    tile_sub_stream_kernel, hand-off, split tail: `bench.py --point-snr 3.0`),
+    at the default bench's frame offset -- counters equal to the static
+    schedule's over the same frames (8 chunks of 32,768), and the frames the
+    supply order puts first (heaviest syndromes: the likely failures) and last
+    decoded by the oracle, frame for frame, equal to the static decoder's."""
+    from ldpc_amd.device import Decoder, Graph
+    code = "wimax_2304_0.5"
+    H = hstd_for(code)
+    g = Graph.cached(H)
+    PF, slots, T = 262144, STEP // 4, 50
+    base = (1 + 3 + 2) * STEP  # bench.py defaults: warmup 1, steps 3, two extra points
+    sg = oracle.sigma_for_snr(3.0)
+    dec = Decoder(g, slots)
+    dec.profile(True)
+    a = dec.mc_run(SEED, [sg], PF, base, T)
+    p = dec.profile_read()
+    dec.profile(False)
+    order = dec.frame_order(SEED, 0, sg, base, PF)
+    dec.close()
+    assert p["tile"][1] == 1 and p["cn"][1] > 0, p  # the supply kernel, then the split tail
+    big = Decoder(g, STEP)
+    b = big.mc_run(SEED, [sg], PF, base, T, static=True)
+    np.testing.assert_array_equal(a, b)
+    assert a[0, 0] == PF and 0 < a[0, 1] < PF // 10  # FER a few per cent at 3 dB
+    # spot check: the first and last 48 frames of the supply order
+    for idx in (order[:48], order[-48:]):
+        us, ls = [], []
+        for i in idx:
+            u, llr = big.generate(SEED, 0, sg, base + int(i), 1)
+            us.append(u[0])
+            ls.append(llr[0])
+        llr = np.stack(ls)
+        r = big.decode(llr, T)
+        o = oracle.spa_decode(H, llr, T)
+        np.testing.assert_array_equal(r.z, o["z"])
+        np.testing.assert_array_equal(r.conv, o["conv"])
+    big.close()
